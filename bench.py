@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""bench.py -- clerk share-combine throughput on MI355X (BASELINE.json metric), plus packed-Shamir
+share-gen / reveal and ChaCha mask-combine side legs.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Step = one exact clerk combine (combiner.rs:16-28) of this rank's 10,000 x 1,000,000 i64 share
+matrix (BASELINE.json configs[1]), HBM-resident before timing starts.  With N > 1 ranks every rank
+combines its own 10k x 1M block (weak scaling: participations shard across GPUs) and the per-rank
+results are summed by one RCCL all-reduce over int64 (== u64 two's complement) and reduced on
+device (sda_amd.distributed).  value = bytes combined by all ranks / max-over-ranks wall time.
+Rank 0 prints ONE JSON line; everything else goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "clerk share-combine GB/s + packed-Shamir shares/s at 1M-dim, 1/2/4/8 GPUs"
+HBM_PEAK_GBPS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
+MODULUS = 2147482801             # m = p = 2147482801
+SEED_BASE = 0x5DA
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=10_000, help="participations per GPU (configs[1]: 10k)")
+    ap.add_argument("--dim", type=int, default=1_000_000, help="vector dimension (configs[1]: 1M)")
+    ap.add_argument("--shamir-vectors", type=int, default=64, help="participant vectors per share-gen launch")
+    ap.add_argument("--chacha-seeds", type=int, default=256)
+    ap.add_argument("--no-side", action="store_true", help="skip packed-Shamir / ChaCha legs")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--only", choices=["combine", "shamir", "chacha"], default=None,
+                    help="profile helper: run just one leg (no JSON contract)")
+    return ap.parse_args()
+
+
+class Timer:
+    """HIP events on torch's current stream -- the stream every engine launch here is issued on."""
+
+    def __init__(self, torch):
+        self.torch = torch
+        self.pairs = []
+
+    def record(self, fn):
+        s = self.torch.cuda.Event(enable_timing=True)
+        e = self.torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        self.pairs.append((s, e))
+
+    def mean_ms(self):
+        self.torch.cuda.synchronize()
+        return statistics.fmean(s.elapsed_time(e) for s, e in self.pairs)
+
+
+def cpu_baseline(dim: int, budget_s: float):
+    """oracle/ C restatement of combiner.rs:16-28 (real `%` per element), 1 core, bounded sample."""
+    from oracle import oracle as O
+    from sda_amd import synth
+    rows = 100
+    x = synth.fill(rows, dim, SEED_BASE + 1, 0, MODULUS)
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < 9 and (time.perf_counter() - t_start) < budget_s or len(times) < 2:
+        t0 = time.perf_counter()
+        O.combine(MODULUS, x)
+        times.append(time.perf_counter() - t0)
+    t = statistics.median(times)
+    return {"value": round(8.0 * rows * dim / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{rows} x {dim:,} i64 rows of the same synthetic matrix (uniform [0, m)), "
+                      f"oracle/sda_oracle.c or_combine at -O2, median of {len(times)} runs"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from sda_amd import Engine, schemes as S
+    from sda_amd import distributed as Dd
+    from sda_amd import engine as E
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    eng = Engine(local)
+    stream = lambda: torch.cuda.current_stream().cuda_stream   # noqa: E731
+    dev = torch.device("cuda", local)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # ---------------- workload: configs[1], HBM-resident ----------------
+    N, D, m = args.rows, args.dim, MODULUS
+    run_combine = args.only in (None, "combine")
+    if run_combine:
+        shares = torch.empty((N, D), dtype=torch.int64, device=dev)
+        eng.synth_fill_dev(shares.data_ptr(), N, D, SEED_BASE + 1 + 1000 * rank, 0, m, stream())
+        partial = torch.empty(D, dtype=torch.int64, device=dev)
+        out = torch.empty(D, dtype=torch.int64, device=dev)
+        ktimer = Timer(torch)
+
+        def step(timed):
+            launch = lambda: eng.combine_dev(m, shares.data_ptr(), N, D, D, partial.data_ptr(), stream())  # noqa
+            if timed:
+                ktimer.record(launch)
+            else:
+                launch()
+            if world > 1:
+                dist.all_reduce(partial, op=dist.ReduceOp.SUM)
+                eng.combine_finalize_dev(m, partial.data_ptr(), D, out.data_ptr(), stream())
+
+        assert Dd.reduce_headroom_ok(world, m)
+        for _ in range(args.warmup):
+            step(False)
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(True)
+        torch.cuda.synchronize()
+        barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        kernel_ms = ktimer.mean_ms()
+        # spot-check the result of the last step against torch's int64 column sums (non-negative inputs)
+        res = out if world > 1 else partial
+        cols = torch.randint(0, D, (4096,), device=dev)
+        ref = torch.remainder(shares[:, cols].sum(dim=0), m)
+        if world > 1:
+            dist.all_reduce(ref, op=dist.ReduceOp.SUM)
+            ref = torch.remainder(ref, m)
+        if not torch.equal(res[cols], ref):
+            raise SystemExit("combine result check FAILED")
+        bytes_per_launch = 8.0 * N * D + 8.0 * D
+        total_bytes = bytes_per_launch * args.steps * world
+        value = total_bytes / dt / 1e9
+        achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+        log(f"[combine] rank {rank}: {args.steps} steps in {dt*1e3:.1f} ms, kernel {kernel_ms:.3f} ms "
+            f"({achieved:.0f} GB/s per launch)")
+        del shares
+
+    # ---------------- side legs (rank-local, reported by rank 0) ----------------
+    side = {}
+    if not args.no_side and args.only in (None, "shamir"):
+        sch = S.CONFIG_PACKED
+        p, k, t, n = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count
+        V, Dm = args.shamir_vectors, 1_000_000
+        B = Dm // k
+        sec = torch.empty((V, Dm), dtype=torch.int64, device=dev)
+        eng.synth_fill_dev(sec.data_ptr(), V, Dm, SEED_BASE + 2, 0, p, stream())
+        drw = torch.empty((V, B, t), dtype=torch.int64, device=dev)
+        eng.synth_fill_dev(drw.data_ptr(), V * B, t, SEED_BASE + 22, 0, p - 1, stream())
+        sh = torch.empty((V, n, B), dtype=torch.int64, device=dev)
+        idx = list(range(n - (t + k), n))           # a t+k clerk subset (result_ready threshold)
+        sub = torch.empty((V, len(idx), B), dtype=torch.int64, device=dev)
+        rev = torch.empty((V, Dm), dtype=torch.int64, device=dev)
+        gen_t, rex_t, rca_t = Timer(torch), Timer(torch), Timer(torch)
+        gen = lambda: eng.packed_generate_dev(sch, sec.data_ptr(), Dm, V, drw.data_ptr(), sh.data_ptr(), stream())  # noqa
+        for i in range(args.warmup + args.steps):
+            gen_t.record(gen) if i >= args.warmup else gen()
+        sub.copy_(sh[:, idx, :])
+        for mode, tm in ((E.REVEAL_EXACT, rex_t), (E.REVEAL_CANONICAL, rca_t)):
+            f = lambda: eng.packed_reconstruct_dev(sch, Dm, idx, V, sub.data_ptr(), rev.data_ptr(), mode, stream())  # noqa
+            for i in range(args.warmup + args.steps):
+                tm.record(f) if i >= args.warmup else f()
+            torch.cuda.synchronize()
+            if not torch.equal(torch.remainder(rev, p), sec):
+                raise SystemExit(f"packed reveal round-trip FAILED (mode {mode})")
+        g_ms, x_ms, c_ms = gen_t.mean_ms(), rex_t.mean_ms(), rca_t.mean_ms()
+        gen_bytes = 8.0 * V * (Dm + t * B + n * B)
+        rev_bytes = 8.0 * V * (len(idx) * B + Dm)
+        side["shamir"] = {
+            "config": "PackedShamir k=8 n=26 t=7 p=2147482801, 1M-dim, %d vectors/launch" % V,
+            "shares_per_s": V * n * B / (g_ms * 1e-3),
+            "gen_ms": g_ms, "gen_GBps": gen_bytes / (g_ms * 1e-3) / 1e9,
+            "gen_roofline_frac": gen_bytes / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "reveal_exact_ms": x_ms, "reveal_exact_GBps": rev_bytes / (x_ms * 1e-3) / 1e9,
+            "reveal_canonical_ms": c_ms, "reveal_canonical_GBps": rev_bytes / (c_ms * 1e-3) / 1e9,
+            "reveal_clerks": len(idx),
+        }
+        log(f"[shamir] {json.dumps(side['shamir'])}")
+        del sec, drw, sh, sub, rev
+    if not args.no_side and args.only in (None, "chacha"):
+        Dc, Ns = 1_000_000, args.chacha_seeds
+        seeds = torch.randint(0, 2**31 - 1, (Ns, 4), dtype=torch.int32, device=dev,
+                              generator=torch.Generator(device=dev).manual_seed(SEED_BASE + 5))
+        cout = torch.empty(Dc, dtype=torch.int64, device=dev)
+        ct = Timer(torch)
+        f = lambda: eng.chacha_mask_combine_dev(m, Dc, seeds.data_ptr(), 4, Ns, cout.data_ptr(), stream())  # noqa
+        for i in range(2 + max(2, args.steps // 4)):
+            ct.record(f) if i >= 2 else f()
+        c_ms = ct.mean_ms()
+        side["chacha"] = {"config": f"ChaCha mask combine, {Ns} seeds x 1M-dim", "ms": c_ms,
+                          "mask_elems_per_s": Ns * Dc / (c_ms * 1e-3),
+                          "chacha_blocks_per_s": Ns * Dc / 8 / (c_ms * 1e-3)}
+        log(f"[chacha] {json.dumps(side['chacha'])}")
+
+    if args.only is not None:
+        return
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic: splitmix64 uniform [0, m) i64 shares, HBM-resident (no checkpoints/datasets)",
+            "config": {"workload": "AdditiveSharing clerk combine, 10k participations x 1M-dim i64 shares per GPU "
+                                   "(BASELINE.json configs[1])",
+                       "participations_per_gpu": N, "dim": D, "modulus": m,
+                       "parallelism": f"participation split x{world}" + (", RCCL int64 all-reduce" if world > 1 else ""),
+                       "exact": "combiner.rs:16-28 recurrence, bit-exact"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profile(N, D)},
+            "kernel_ms": round(kernel_ms, 4),
+        }
+        rec.update(side)
+        if world == 1 and not args.no_cpu:
+            rec["cpu_baseline"] = cpu_baseline(D, args.cpu_seconds)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def traffic_from_profile(N, D):
+    """HBM bytes per combine launch from the committed rocprofv3 PMC pass (profiles/), if it was
+    collected for this exact workload; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM."""
+    path = os.path.join(ROOT, "profiles", "combine_traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("rows") == N and t.get("dim") == D:
+            return t["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+if __name__ == "__main__":
+    main()

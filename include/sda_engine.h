@@ -1,0 +1,198 @@
+/*
+ * sda_engine.h -- C ABI of the MI355X (gfx950) SDA secret-sharing engine.
+ *
+ * This is the drop-in boundary for the reference client's sharing and masking
+ * traits (baajur/sda, client/src/crypto/{sharing,masking}/mod.rs).  A Rust FFI
+ * shim implements the six traits on top of these entry points
+ * and is selected in the factories at client/src/crypto/sharing/mod.rs:35-96
+ * and client/src/crypto/masking/mod.rs:33-94.
+ *
+ * Conventions
+ *   - Elements are i64 (client/src/crypto/mod.rs:33-36); arithmetic follows
+ *     Rust: truncated `%`, wrapping `+` (release builds).
+ *   - The caller owns every buffer.  Host entry points are synchronous (they
+ *     return when results are in host memory), like the Rust trait calls.
+ *   - Entry points suffixed `_dev` take DEVICE pointers and a hipStream_t
+ *     (passed as void*; NULL = the HIP null stream, the same convention as the
+ *     ROCm math libraries); they only enqueue work, except that the ChaCha
+ *     combine waits for its rejection log (a few bytes) before returning.
+ *   - Randomness is explicit.  Where the reference draws from OsRng the caller
+ *     passes the drawn values (or, for ChaCha masking, the seed words).
+ *   - Every function returns an sda_status; 0 = OK.  The codes 1..6 map 1:1 to
+ *     the reference's error strings; sda_last_error_message() gives details.
+ *   - A handle may be used from one thread at a time (the Rust trait objects
+ *     are not Sync either); distinct handles are independent.
+ */
+#ifndef SDA_ENGINE_H
+#define SDA_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDA_ENGINE_ABI_VERSION 1
+
+typedef enum {
+    SDA_OK = 0,
+    SDA_ERR_BATCH_INPUT_WRONG_LENGTH = 1,     /* "Batch input wrong length"          additive.rs:33      */
+    SDA_ERR_PACKED_SHARING_FAILED = 2,        /* "Sharing failed for packed secret sharing scheme" packed_shamir.rs:41 */
+    SDA_ERR_WRONG_DIMENSION = 3,              /* "Wrong dimension"                   combiner.rs:21      */
+    SDA_ERR_MISMATCHING_DIMENSION = 4,        /* "Mismatching dimension"             additive.rs:64      */
+    SDA_ERR_INPUTS_MUST_HAVE_SAME_LENGTH = 5, /* "Inputs must have same length"      packed_shamir.rs:74 */
+    SDA_ERR_NOT_ENOUGH_SHARES = 6,            /* "Not enough shares to reconstruct"  packed_shamir.rs:75 */
+    SDA_ERR_PRECONDITION = 64,   /* where the reference panics (assert!/assert_eq!, chacha.rs:26 ...)   */
+    SDA_ERR_INVALID_ARGUMENT = 65, /* null handle/pointer, buffer too small                              */
+    SDA_ERR_UNSUPPORTED = 66,    /* scheme parameters outside the engine's domain       */
+    SDA_ERR_DEVICE = 67,         /* HIP runtime / kernel failure                                        */
+    SDA_ERR_OUT_OF_MEMORY = 68
+} sda_status;
+
+/* protocol/src/crypto.rs:79-114  LinearSecretSharingScheme */
+typedef enum { SDA_SHARING_ADDITIVE = 0, SDA_SHARING_PACKED_SHAMIR = 1 } sda_sharing_kind;
+typedef struct {
+    int32_t kind;                /* sda_sharing_kind                                  */
+    uint64_t share_count;        /* Additive.share_count / PackedShamir.share_count   */
+    int64_t modulus;             /* Additive.modulus     / PackedShamir.prime_modulus */
+    uint64_t secret_count;       /* PackedShamir only                                 */
+    uint64_t privacy_threshold;  /* PackedShamir only                                 */
+    int64_t omega_secrets;       /* PackedShamir only                                 */
+    int64_t omega_shares;        /* PackedShamir only                                 */
+} sda_sharing_scheme;
+
+/* protocol/src/crypto.rs:43-64  LinearMaskingScheme */
+typedef enum { SDA_MASKING_NONE = 0, SDA_MASKING_FULL = 1, SDA_MASKING_CHACHA = 2 } sda_masking_kind;
+typedef struct {
+    int32_t kind;                /* sda_masking_kind                    */
+    int64_t modulus;             /* Full.modulus / ChaCha.modulus       */
+    uint64_t dimension;          /* ChaCha.dimension                    */
+    uint64_t seed_bitsize;       /* ChaCha.seed_bitsize                 */
+} sda_masking_scheme;
+
+/* Packed-Shamir reveal representation. */
+typedef enum {
+    SDA_REVEAL_EXACT = 0,        /* bit-exact signed representatives of tss reconstruct (Newton) */
+    SDA_REVEAL_CANONICAL = 1     /* canonical residues in [0,p) (Lagrange weights); equal mod p  */
+} sda_reveal_mode;
+
+typedef struct sda_engine sda_engine;
+
+/* ---------------- lifecycle / diagnostics ---------------- */
+int sda_abi_version(void);
+sda_status sda_engine_create(int device_ordinal, sda_engine** out);
+void sda_engine_destroy(sda_engine* h);
+sda_status sda_engine_synchronize(sda_engine* h);
+const char* sda_last_error_message(void);          /* thread-local; never NULL */
+const char* sda_status_string(int status);         /* reference error string for 1..6 */
+
+/* ---------------- derived scheme sizes: protocol/src/crypto.rs:117-155 ---------------- */
+uint64_t sda_scheme_input_size(const sda_sharing_scheme* s);              /* :120-126 */
+uint64_t sda_scheme_output_size(const sda_sharing_scheme* s);             /* :129-135 */
+uint64_t sda_scheme_privacy_threshold(const sda_sharing_scheme* s);       /* :138-144 */
+uint64_t sda_scheme_reconstruction_threshold(const sda_sharing_scheme* s);/* :147-153 */
+/* number of batches per clerk vector: ceil(dimension / input_size) (batched.rs:21-23) */
+uint64_t sda_share_length(const sda_sharing_scheme* s, uint64_t dimension);
+
+/* ---------------- trait mirrors (host buffers, synchronous) ---------------- */
+
+/* ShareGenerator::generate  (sharing/mod.rs:14-17; batched.rs:19-53)
+ *   secrets[dimension];  draws: the values OsRng produced, in draw order:
+ *     Additive     [dimension][share_count-1]   gen_range(0, modulus)   additive.rs:42-44
+ *     PackedShamir [B][privacy_threshold]       tss Range(0, p-1) sample
+ *   out: [share_count][B] clerk-major, B = sda_share_length(s, dimension). */
+sda_status sda_share_generate(sda_engine* h, const sda_sharing_scheme* s,
+                              const int64_t* secrets, uint64_t dimension,
+                              const int64_t* draws, uint64_t n_draws,
+                              int64_t* out, uint64_t out_cap);
+
+/* ShareCombiner::combine  (sharing/mod.rs:23-25; combiner.rs:16-28)
+ *   rows[i] has lens[i] elements (a Vec<Vec<i64>>).  out_len = lens[0] (0 if n_rows == 0). */
+sda_status sda_share_combine(sda_engine* h, const sda_sharing_scheme* s,
+                             const int64_t* const* rows, const uint64_t* lens, uint64_t n_rows,
+                             int64_t* out, uint64_t out_cap, uint64_t* out_len);
+
+/* SecretReconstructor::reconstruct  (sharing/mod.rs:31-33; additive.rs:56-72; batched.rs:69-97)
+ *   indexed shares = (indices[i], rows[i][lens[i]]);  dimension = factory argument (mod.rs:76). */
+sda_status sda_secret_reconstruct(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,
+                                  const uint64_t* indices, const int64_t* const* rows,
+                                  const uint64_t* lens, uint64_t n_rows,
+                                  int64_t* out, uint64_t out_cap, uint64_t* out_len);
+
+/* SecretMasker::mask  (masking/mod.rs:13-15)
+ *   None:   mask_len = 0, masked = secrets                        (none.rs:14-19)
+ *   Full:   full_masks[dimension] = the OsRng draws; mask = them  (full.rs:22-35)
+ *   ChaCha: seed[seed_words] = the OsRng seed words; mask = seed as i64 (chacha.rs:25-53)
+ *   mask_out needs room for dimension (Full) or seed_words (ChaCha) values. */
+sda_status sda_secret_mask(sda_engine* h, const sda_masking_scheme* s,
+                           const int64_t* secrets, uint64_t dimension,
+                           const uint32_t* seed, uint64_t seed_words,
+                           const int64_t* full_masks,
+                           int64_t* mask_out, uint64_t mask_cap, uint64_t* mask_len,
+                           int64_t* masked_out);
+
+/* MaskCombiner::combine  (masking/mod.rs:21-23)
+ *   Full: rows are masks (full.rs:38-50); ChaCha: rows are seeds-as-i64 (chacha.rs:57-76);
+ *   None: every row must be empty, out_len = 0 (none.rs:22-25). */
+sda_status sda_mask_combine(sda_engine* h, const sda_masking_scheme* s,
+                            const int64_t* const* rows, const uint64_t* lens, uint64_t n_rows,
+                            int64_t* out, uint64_t out_cap, uint64_t* out_len);
+
+/* SecretUnmasker::unmask  (masking/mod.rs:29-31; chacha.rs:80-91; full.rs:55-66; none.rs:28-32)
+ *   For ChaCha, `mask` is the COMBINED mask (the recipient's mask_combiner output). */
+sda_status sda_secret_unmask(sda_engine* h, const sda_masking_scheme* s,
+                             const int64_t* mask, uint64_t mask_len,
+                             const int64_t* masked, uint64_t masked_len,
+                             int64_t* out, uint64_t out_cap, uint64_t* out_len);
+
+/* RecipientOutput::positive  (receive.rs:14-20) */
+sda_status sda_recipient_positive(sda_engine* h, int64_t modulus, const int64_t* values,
+                                  uint64_t n, int64_t* out);
+
+/* ---------------- device-resident entry points (HBM-resident inputs) ---------------- */
+
+/* Exact clerk combine of a dense [n][dim] matrix with row stride `row_stride` elements:
+ * out[j] = combiner.rs:22-25 applied over rows 0..n-1 in order. */
+sda_status sda_combine_dev(sda_engine* h, int64_t modulus, const int64_t* shares,
+                           uint64_t n, uint64_t dim, uint64_t row_stride,
+                           int64_t* out, void* stream);
+
+/* Multi-GPU finalize: `sums` are the two's-complement u64 sums (RCCL-reduced) of per-GPU
+ * combine results; out = canonical residue in [0, m).  Exact w.r.t. the reference when all
+ * combined inputs were non-negative (DESIGN.md "multi-GPU"). */
+sda_status sda_combine_finalize_dev(sda_engine* h, int64_t modulus, const int64_t* sums,
+                                    uint64_t dim, int64_t* out, void* stream);
+
+/* Packed-Shamir share generation for `n_vectors` participant vectors at once:
+ * secrets [n_vectors][dimension], draws [n_vectors][B][t], out [n_vectors][n][B]. */
+sda_status sda_packed_generate_dev(sda_engine* h, const sda_sharing_scheme* s,
+                                   const int64_t* secrets, uint64_t dimension, uint64_t n_vectors,
+                                   const int64_t* draws, int64_t* out, void* stream);
+
+/* Packed-Shamir reveal: shares [n_vectors][n_idx][B] at clerk `indices` (host array),
+ * out [n_vectors][dimension]. */
+sda_status sda_packed_reconstruct_dev(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,
+                                      const uint64_t* indices, uint64_t n_idx, uint64_t n_vectors,
+                                      const int64_t* shares, int64_t* out, int32_t mode, void* stream);
+
+/* Additive share generation: secrets [dimension], draws [dimension][n-1], out [n][dimension]. */
+sda_status sda_additive_generate_dev(sda_engine* h, int64_t modulus, uint64_t share_count,
+                                     const int64_t* secrets, uint64_t dimension,
+                                     const int64_t* draws, int64_t* out, void* stream);
+
+/* ChaCha mask expansion + combine (chacha.rs:57-76) over n_seeds seeds of w words
+ * (seeds [n_seeds][w] u32, device), out [dimension] canonical.  Exact including
+ * gen_range rejections (handled by an on-device fix-up pass). */
+sda_status sda_chacha_mask_combine_dev(sda_engine* h, int64_t modulus, uint64_t dimension,
+                                       const uint32_t* seeds, uint64_t w, uint64_t n_seeds,
+                                       int64_t* out, void* stream);
+
+/* Synthetic benchmark input: dst[r*cols + c] = lo + splitmix64(seed, r, c) % (hi - lo). */
+sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64_t cols,
+                              uint64_t seed, int64_t lo, int64_t hi, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDA_ENGINE_H */

@@ -1,0 +1,262 @@
+// chacha.hip -- north-star kernel (3): ChaCha PRG mask expansion in counter mode.
+//
+// Reference: client/src/crypto/masking/chacha.rs
+//   mask     :25-53  ChaChaRng::from_seed(seed); D x gen_range(0, m); masked = (s + mask) % m
+//   combine  :57-76  for each participant seed: re-seed, D x gen_range, result = (r + m) % m
+// rand 0.3 (absent from the reference tree) defines the stream: ChaCha20 (10 double rounds),
+// state = "expand 32-byte k" | key = seed words (zero-padded, first 8) | 128-bit block counter
+// from 0; next_u64 = (next_u32 << 32) | next_u32; gen_range(0, m) draws v = next_u64 and
+// rejects v >= zone = u64::MAX - u64::MAX % m, else returns v % m.
+//
+// Counter mode makes the stream randomly accessible: absent rejections, element i of a stream
+// is words (2i, 2i+1) = block i/8.  One lane expands one 64-byte block (8 mask elements) per
+// seed and loops over seeds, accumulating canonical sums (every draw is >= 0, so the reference
+// result is the canonical sum and order-independent).  A rejection shifts every later element
+// of that stream by one word pair: the main kernel adds the un-shifted draw and records the
+// (seed, pair) event; a host-driven fix-up then recomputes only the affected stream suffixes
+// (probability < 2^-33 per draw for 31-bit m).  Roofline: VALU (~1000 int32 ops per block).
+#include <algorithm>
+#include <vector>
+
+#include "kernels.h"
+
+namespace sda {
+
+namespace {
+
+constexpr uint32_t C0 = 0x61707865u, C1 = 0x3320646Eu, C2 = 0x79622D32u, C3 = 0x6B206574u;
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return __builtin_amdgcn_alignbit(x, x, 32 - r); }
+
+#define SDA_QR(a, b, c, d)                    \
+    a += b; d ^= a; d = rotl(d, 16);          \
+    c += d; b ^= c; b = rotl(b, 12);          \
+    a += b; d ^= a; d = rotl(d, 8);           \
+    c += d; b ^= c; b = rotl(b, 7);
+
+struct Key8 { uint32_t k[8]; };
+
+// one ChaCha20 block: core(state) = rounds(state) + state
+__device__ __forceinline__ void chacha_block(const uint32_t* key, uint64_t counter, uint32_t (&o)[16]) {
+    uint32_t x0 = C0, x1 = C1, x2 = C2, x3 = C3;
+    uint32_t x4 = key[0], x5 = key[1], x6 = key[2], x7 = key[3];
+    uint32_t x8 = key[4], x9 = key[5], x10 = key[6], x11 = key[7];
+    uint32_t x12 = (uint32_t)counter, x13 = (uint32_t)(counter >> 32), x14 = 0, x15 = 0;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        SDA_QR(x0, x4, x8, x12); SDA_QR(x1, x5, x9, x13); SDA_QR(x2, x6, x10, x14); SDA_QR(x3, x7, x11, x15);
+        SDA_QR(x0, x5, x10, x15); SDA_QR(x1, x6, x11, x12); SDA_QR(x2, x7, x8, x13); SDA_QR(x3, x4, x9, x14);
+    }
+    o[0] = x0 + C0; o[1] = x1 + C1; o[2] = x2 + C2; o[3] = x3 + C3;
+    o[4] = x4 + key[0]; o[5] = x5 + key[1]; o[6] = x6 + key[2]; o[7] = x7 + key[3];
+    o[8] = x8 + key[4]; o[9] = x9 + key[5]; o[10] = x10 + key[6]; o[11] = x11 + key[7];
+    o[12] = x12 + (uint32_t)counter; o[13] = x13 + (uint32_t)(counter >> 32); o[14] = x14; o[15] = x15;
+}
+
+struct RejectLog {
+    unsigned long long* count;   // number of rejected pairs seen
+    uint32_t* seed_of;           // [cap]
+    uint64_t* pair_of;           // [cap]
+    uint64_t cap;
+};
+
+// acc[i] += sum over seeds in this y-chunk of draw_i  (un-shifted), canonical per chunk
+__global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __restrict__ seeds, uint32_t w,
+                                                             uint64_t n_seeds, uint64_t seeds_per_chunk,
+                                                             uint64_t D, unsigned long long* __restrict__ acc,
+                                                             Mod64 M, uint64_t zone, RejectLog log) {
+    const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t n_blk = (D + 7) / 8;
+    if (blk >= n_blk) return;
+    const uint64_t s0 = (uint64_t)blockIdx.y * seeds_per_chunk;
+    const uint64_t s1 = s0 + seeds_per_chunk < n_seeds ? s0 + seeds_per_chunk : n_seeds;
+    const uint32_t nw = w < 8 ? w : 8;
+    const uint64_t m = M.m;
+    uint64_t a[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a[q] = 0;
+    for (uint64_t s = s0; s < s1; ++s) {
+        uint32_t key[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) key[q] = (uint32_t)q < nw ? seeds[s * w + q] : 0u;   // uniform: scalar loads
+        uint32_t o[16];
+        chacha_block(key, blk, o);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t v = ((uint64_t)o[2 * q] << 32) | o[2 * q + 1];    // high word first
+            const uint64_t pair = blk * 8 + q;
+            if (pair < D) {
+                if (v >= zone) {                                            // rejected: log it
+                    const unsigned long long slot = atomicAdd(log.count, 1ull);
+                    if (slot < log.cap) { log.seed_of[slot] = (uint32_t)s; log.pair_of[slot] = pair; }
+                }
+                uint64_t x = a[q] + umod64(v, M);
+                a[q] = x >= m ? x - m : x;
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        if (blk * 8 + q < D) atomicAdd(&acc[blk * 8 + q], (unsigned long long)a[q]);
+}
+
+// Fix one stream: for elements i >= i0, replace draw(pair i) by draw(pair a_i), where a_i is the
+// i-th non-rejected pair: a_i = i + #{r in rej : r <= a_i}.  acc stays unsigned: += new + m - old.
+__global__ __launch_bounds__(256) void chacha_fix_kernel(Key8 key, uint64_t i0, uint64_t D,
+                                                         const uint64_t* __restrict__ rej, uint32_t n_rej,
+                                                         unsigned long long* __restrict__ acc, Mod64 M) {
+    const uint64_t i = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= D) return;
+    auto count_le = [&](uint64_t x) -> uint64_t {   // #{r <= x}
+        uint32_t lo = 0, hi = n_rej;
+        while (lo < hi) { uint32_t mid = (lo + hi) / 2; if (rej[mid] <= x) lo = mid + 1; else hi = mid; }
+        return lo;
+    };
+    uint64_t k = count_le(i);
+    for (;;) { const uint64_t k2 = count_le(i + k); if (k2 == k) break; k = k2; }
+    const uint64_t ai = i + k;
+    uint32_t o[16];
+    chacha_block(key.k, i / 8, o);
+    const uint64_t vo = ((uint64_t)o[2 * (i % 8)] << 32) | o[2 * (i % 8) + 1];
+    chacha_block(key.k, ai / 8, o);
+    const uint64_t vn = ((uint64_t)o[2 * (ai % 8)] << 32) | o[2 * (ai % 8) + 1];
+    acc[i] += (unsigned long long)(umod64(vn, M) + (M.m - umod64(vo, M)));
+}
+
+__global__ __launch_bounds__(256) void acc_mod_kernel(const unsigned long long* __restrict__ acc, uint64_t D,
+                                                      int64_t* __restrict__ out, Mod64 M) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < D) out[i] = (int64_t)umod64(acc[i], M);
+}
+
+// ---- host ChaCha (product code: extends a stream's rejection list past D) ----
+inline uint32_t h_rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+void h_block(const uint32_t* key, uint64_t counter, uint32_t o[16]) {
+    uint32_t in[16] = {C0, C1, C2, C3, key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7],
+                       (uint32_t)counter, (uint32_t)(counter >> 32), 0, 0};
+    uint32_t x[16];
+    for (int i = 0; i < 16; ++i) x[i] = in[i];
+#define H_QR(a, b, c, d) \
+    x[a] += x[b]; x[d] ^= x[a]; x[d] = h_rotl(x[d], 16); x[c] += x[d]; x[b] ^= x[c]; x[b] = h_rotl(x[b], 12); \
+    x[a] += x[b]; x[d] ^= x[a]; x[d] = h_rotl(x[d], 8);  x[c] += x[d]; x[b] ^= x[c]; x[b] = h_rotl(x[b], 7);
+    for (int r = 0; r < 10; ++r) {
+        H_QR(0, 4, 8, 12) H_QR(1, 5, 9, 13) H_QR(2, 6, 10, 14) H_QR(3, 7, 11, 15)
+        H_QR(0, 5, 10, 15) H_QR(1, 6, 11, 12) H_QR(2, 7, 8, 13) H_QR(3, 4, 9, 14)
+    }
+#undef H_QR
+    for (int i = 0; i < 16; ++i) o[i] = x[i] + in[i];
+}
+uint64_t h_pair(const uint32_t* key, uint64_t pair) {
+    uint32_t o[16];
+    h_block(key, pair / 8, o);
+    return ((uint64_t)o[2 * (pair % 8)] << 32) | o[2 * (pair % 8) + 1];
+}
+
+}  // namespace
+
+// work layout: [acc: D u64][count u64][seed_of: cap u32][pair_of: cap u64][rej upload: cap u64]
+static constexpr uint64_t kRejectCap = 1 << 16;
+
+size_t chacha_work_bytes(uint64_t dimension) {
+    return dimension * 8 + 16 + kRejectCap * (4 + 8 + 8) + 64;
+}
+
+static hipError_t chacha_combine_impl(int64_t modulus, uint64_t D, const uint32_t* seeds_dev,
+                                      const std::vector<uint32_t>& seeds_host, uint32_t w, uint64_t n_seeds,
+                                      int64_t* out, void* work, hipStream_t s, int* fixups_out) {
+    if (fixups_out) *fixups_out = 0;
+    if (D == 0) return hipSuccess;
+    const Mod64 M = make_mod64(modulus);
+    const uint64_t zone = UINT64_MAX - UINT64_MAX % (uint64_t)modulus;
+    char* base = static_cast<char*>(work);
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(base);
+    unsigned long long* count = reinterpret_cast<unsigned long long*>(base + D * 8);
+    uint32_t* seed_of = reinterpret_cast<uint32_t*>(base + D * 8 + 16);
+    uint64_t* pair_of = reinterpret_cast<uint64_t*>(base + D * 8 + 16 + kRejectCap * 4);
+    uint64_t* rej_up = pair_of + kRejectCap;
+    hipError_t e;
+    if ((e = hipMemsetAsync(acc, 0, D * 8 + 16, s)) != hipSuccess) return e;
+
+    const uint64_t n_blk = (D + 7) / 8;
+    const uint64_t gx = (n_blk + 255) / 256;
+    // enough workgroups to fill 256 CUs x 8 waves; split seeds over grid.y
+    uint64_t chunks = (2048 + gx - 1) / gx;
+    if (chunks > n_seeds) chunks = n_seeds ? n_seeds : 1;
+    if (chunks > 65535) chunks = 65535;
+    const uint64_t per = n_seeds ? (n_seeds + chunks - 1) / chunks : 0;
+    RejectLog log{count, seed_of, pair_of, kRejectCap};
+    if (n_seeds) {
+        hipLaunchKernelGGL(chacha_combine_kernel, dim3((unsigned)gx, (unsigned)chunks), dim3(256), 0, s, seeds_dev, w,
+                           n_seeds, per, D, acc, M, zone, log);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        // read the rejection log (a few bytes) -- the call is synchronous anyway
+        unsigned long long n_rej = 0;
+        if ((e = hipMemcpyAsync(&n_rej, count, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (n_rej > kRejectCap) return hipErrorOutOfMemory;   // engine falls back (see engine.cpp)
+        if (n_rej) {
+            std::vector<uint32_t> so(n_rej);
+            std::vector<uint64_t> po(n_rej);
+            if ((e = hipMemcpy(so.data(), seed_of, n_rej * 4, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+            if ((e = hipMemcpy(po.data(), pair_of, n_rej * 8, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+            std::vector<std::pair<uint32_t, uint64_t>> ev(n_rej);
+            for (size_t i = 0; i < n_rej; ++i) ev[i] = {so[i], po[i]};
+            std::sort(ev.begin(), ev.end());
+            const uint32_t nw = w < 8 ? w : 8;
+            size_t i = 0;
+            while (i < ev.size()) {
+                const uint32_t sd = ev[i].first;
+                std::vector<uint64_t> rej;
+                while (i < ev.size() && ev[i].first == sd) rej.push_back(ev[i++].second);
+                Key8 key{};
+                for (uint32_t q = 0; q < nw; ++q) key.k[q] = seeds_host[(size_t)sd * w + q];
+                // extend past D: pairs D .. D + |rej| - 1 (+ any further rejections there)
+                uint64_t scanned = D;
+                while (scanned < D + rej.size()) {
+                    const uint64_t v = h_pair(key.k, scanned);
+                    if (v >= zone) rej.push_back(scanned);
+                    ++scanned;
+                }
+                if (rej.size() > kRejectCap) return hipErrorOutOfMemory;
+                if ((e = hipMemcpy(rej_up, rej.data(), rej.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return e;
+                const uint64_t i0 = rej.front();
+                const uint64_t nfix = D - i0;
+                hipLaunchKernelGGL(chacha_fix_kernel, dim3((unsigned)((nfix + 255) / 256)), dim3(256), 0, s, key, i0, D,
+                                   rej_up, (uint32_t)rej.size(), acc, M);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+                if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;   // rej_up is reused
+                if (fixups_out) ++*fixups_out;
+            }
+        }
+    }
+    hipLaunchKernelGGL(acc_mod_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, acc, D, out, M);
+    return hipGetLastError();
+}
+
+hipError_t launch_chacha_mask_combine(int64_t modulus, uint64_t dimension, const uint32_t* seeds, uint32_t w,
+                                      uint64_t n_seeds, int64_t* out, void* work, hipStream_t s, int* fixups_out) {
+    // host copy of the seeds, needed only if a rejection occurs (tiny: n_seeds * w words)
+    std::vector<uint32_t> host((size_t)n_seeds * w);
+    if (!host.empty()) {
+        hipError_t e = hipMemcpyAsync(host.data(), seeds, host.size() * 4, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return e;
+    }
+    return chacha_combine_impl(modulus, dimension, seeds, host, w, n_seeds, out, work, s, fixups_out);
+}
+
+hipError_t launch_chacha_mask(int64_t modulus, const uint32_t* seed_host, uint32_t w, const int64_t* secrets,
+                              uint64_t D, int64_t* masked, void* work, hipStream_t s) {
+    // mask_i = single-stream "combine"; masked = (s + mask) % m  (chacha.rs:42-45)
+    std::vector<uint32_t> host(seed_host, seed_host + w);
+    char* base = static_cast<char*>(work);
+    const size_t need = chacha_work_bytes(D);
+    uint32_t* seed_dev = reinterpret_cast<uint32_t*>(base + need);
+    int64_t* mask_dev = reinterpret_cast<int64_t*>(base + need + 64);
+    hipError_t e;
+    if (w && (e = hipMemcpyAsync(seed_dev, seed_host, w * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = chacha_combine_impl(modulus, D, seed_dev, host, w, 1, mask_dev, work, s, nullptr)) != hipSuccess)
+        return e;
+    return launch_addsub_trem(secrets, mask_dev, +1, D, masked, modulus, s);
+}
+
+}  // namespace sda

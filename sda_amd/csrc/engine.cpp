@@ -1,0 +1,592 @@
+// engine.cpp -- C ABI of the MI355X SDA engine (include/sda_engine.h).
+//
+// Host-side responsibilities only: argument validation with the reference's error behaviour
+// (Err strings of client/src/crypto/sharing/*.rs -> status 1..6, assert!/panic -> PRECONDITION),
+// staging of host buffers to HBM, kernel launches (kernels.h) and copying results back.  No
+// arithmetic on the data happens here and there is no CPU fallback: if the device path fails
+// the call fails.
+#include "../../include/sda_engine.h"
+
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+struct sda_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    void* work = nullptr;
+    size_t work_bytes = 0;
+    void* stage = nullptr;        // staging for host-path inputs/outputs
+    size_t stage_bytes = 0;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+sda_status fail(sda_status st, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return st;
+}
+
+sda_status ok() {
+    g_last_error.clear();
+    return SDA_OK;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess)                                                                      \
+            return fail(_e == hipErrorOutOfMemory ? SDA_ERR_OUT_OF_MEMORY : SDA_ERR_DEVICE,        \
+                        "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+    } while (0)
+
+sda_status ensure(void** buf, size_t* have, size_t need) {
+    if (need <= *have) return SDA_OK;
+    if (*buf) (void)hipFree(*buf);
+    *buf = nullptr;
+    *have = 0;
+    size_t want = need + need / 4 + 4096;
+    HIP_TRY(hipMalloc(buf, want));
+    *have = want;
+    return SDA_OK;
+}
+
+// `_dev` entry points run on the caller's stream; NULL is the HIP null (default) stream, which is
+// also what torch's default stream reports -- so work stays ordered with the caller's own ops.
+hipStream_t pick(sda_engine*, void* stream) { return static_cast<hipStream_t>(stream); }
+
+bool is_pow(uint64_t x, uint64_t b) {
+    if (x < 1) return false;
+    while (x % b == 0) x /= b;
+    return x == 1;
+}
+
+// Rust `x % m` with m < 0 equals `x % |m|`; m == 0 panics.
+sda_status modulus_abs(int64_t m, int64_t* out) {
+    if (m == 0) return fail(SDA_ERR_PRECONDITION, "attempt to calculate the remainder with a divisor of zero");
+    if (m == INT64_MIN) return fail(SDA_ERR_UNSUPPORTED, "modulus i64::MIN is outside the engine's domain");
+    *out = m < 0 ? -m : m;
+    return SDA_OK;
+}
+
+// Packed-Shamir parameter domain of the engine (DESIGN.md "Domain").
+sda_status check_packed(const sda_sharing_scheme* s) {
+    const uint64_t k = s->secret_count, t = s->privacy_threshold, n = s->share_count;
+    const int64_t p = s->modulus;
+    if (k == 0) return fail(SDA_ERR_UNSUPPORTED, "secret_count must be >= 1");
+    if (n + 1 < k + t + 1)   // tss: vec![0; share_count - reconstruct_limit()] underflows
+        return fail(SDA_ERR_PRECONDITION, "share_count (%llu) < secret_count + privacy_threshold (%llu)",
+                    (unsigned long long)n, (unsigned long long)(k + t));
+    if (!is_pow(k + t + 1, 2) || k + t + 1 > 64)
+        return fail(SDA_ERR_UNSUPPORTED, "secret_count + privacy_threshold + 1 = %llu must be a power of 2 <= 64",
+                    (unsigned long long)(k + t + 1));
+    if (!is_pow(n + 1, 3) || n + 1 > 81)
+        return fail(SDA_ERR_UNSUPPORTED, "share_count + 1 = %llu must be a power of 3 <= 81",
+                    (unsigned long long)(n + 1));
+    if (p < 3 || p % 2 == 0 || p >= ((int64_t)1 << 31))
+        return fail(SDA_ERR_UNSUPPORTED, "prime_modulus %lld must be odd and < 2^31 (tss i64 headroom)",
+                    (long long)p);
+    if (s->omega_secrets <= 0 || s->omega_secrets >= p || s->omega_shares <= 0 || s->omega_shares >= p)
+        return fail(SDA_ERR_UNSUPPORTED, "omega_secrets / omega_shares must lie in (0, p)");
+    return SDA_OK;
+}
+
+// upload n rows of `len` elements each into a dense [n][len] device buffer
+sda_status upload_rows(sda_engine* h, int64_t* dst, const int64_t* const* rows, uint64_t n, uint64_t len) {
+    uint64_t i = 0;
+    while (i < n) {
+        uint64_t j = i + 1;   // coalesce rows that are contiguous in host memory
+        while (j < n && rows[j] == rows[j - 1] + len) ++j;
+        if (len) HIP_TRY(hipMemcpyAsync(dst + i * len, rows[i], (j - i) * len * 8, hipMemcpyHostToDevice, h->stream));
+        i = j;
+    }
+    return SDA_OK;
+}
+
+struct DevArena {   // bump allocator over the engine's staging buffer
+    char* base;
+    size_t off = 0;
+    template <typename T> T* take(size_t count) {
+        T* p = reinterpret_cast<T*>(base + off);
+        off += (count * sizeof(T) + 255) & ~(size_t)255;
+        return p;
+    }
+};
+
+sda_status stage(sda_engine* h, size_t bytes, DevArena* a) {
+    sda_status st = ensure(&h->stage, &h->stage_bytes, bytes + 4096);
+    if (st) return st;
+    a->base = static_cast<char*>(h->stage);
+    a->off = 0;
+    return SDA_OK;
+}
+
+size_t rup(size_t b) { return (b + 255) & ~(size_t)255; }
+
+sda_status finish(sda_engine* h) {
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return ok();
+}
+
+}  // namespace
+
+extern "C" {
+
+int sda_abi_version(void) { return SDA_ENGINE_ABI_VERSION; }
+
+const char* sda_last_error_message(void) { return g_last_error.c_str(); }
+
+const char* sda_status_string(int st) {
+    switch (st) {
+        case SDA_OK: return "ok";
+        case SDA_ERR_BATCH_INPUT_WRONG_LENGTH: return "Batch input wrong length";
+        case SDA_ERR_PACKED_SHARING_FAILED: return "Sharing failed for packed secret sharing scheme";
+        case SDA_ERR_WRONG_DIMENSION: return "Wrong dimension";
+        case SDA_ERR_MISMATCHING_DIMENSION: return "Mismatching dimension";
+        case SDA_ERR_INPUTS_MUST_HAVE_SAME_LENGTH: return "Inputs must have same length";
+        case SDA_ERR_NOT_ENOUGH_SHARES: return "Not enough shares to reconstruct";
+        case SDA_ERR_PRECONDITION: return "precondition violated (the reference panics here)";
+        case SDA_ERR_INVALID_ARGUMENT: return "invalid argument";
+        case SDA_ERR_UNSUPPORTED: return "unsupported parameters";
+        case SDA_ERR_DEVICE: return "device error";
+        case SDA_ERR_OUT_OF_MEMORY: return "out of device memory";
+    }
+    return "unknown status";
+}
+
+sda_status sda_engine_create(int device_ordinal, sda_engine** out) {
+    if (!out) return fail(SDA_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device_ordinal < 0 || device_ordinal >= n)
+        return fail(SDA_ERR_INVALID_ARGUMENT, "device %d out of range (%d devices)", device_ordinal, n);
+    HIP_TRY(hipSetDevice(device_ordinal));
+    sda_engine* h = new sda_engine();
+    h->device = device_ordinal;
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete h;
+        return fail(SDA_ERR_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    *out = h;
+    return ok();
+}
+
+void sda_engine_destroy(sda_engine* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->work) (void)hipFree(h->work);
+    if (h->stage) (void)hipFree(h->stage);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+sda_status sda_engine_synchronize(sda_engine* h) {
+    if (!h) return fail(SDA_ERR_INVALID_ARGUMENT, "engine handle is NULL");
+    HIP_TRY(hipDeviceSynchronize());
+    return ok();
+}
+
+// ---------------- protocol/src/crypto.rs:117-155 ----------------
+uint64_t sda_scheme_input_size(const sda_sharing_scheme* s) {
+    return s->kind == SDA_SHARING_ADDITIVE ? 1 : s->secret_count;
+}
+uint64_t sda_scheme_output_size(const sda_sharing_scheme* s) { return s->share_count; }
+uint64_t sda_scheme_privacy_threshold(const sda_sharing_scheme* s) {
+    return s->kind == SDA_SHARING_ADDITIVE ? s->share_count - 1 : s->privacy_threshold;
+}
+uint64_t sda_scheme_reconstruction_threshold(const sda_sharing_scheme* s) {
+    return s->kind == SDA_SHARING_ADDITIVE ? s->share_count : s->privacy_threshold + s->secret_count;
+}
+uint64_t sda_share_length(const sda_sharing_scheme* s, uint64_t dimension) {
+    const uint64_t k = sda_scheme_input_size(s);
+    return k ? (dimension + k - 1) / k : 0;
+}
+
+// ---------------- ShareGenerator::generate ----------------
+sda_status sda_share_generate(sda_engine* h, const sda_sharing_scheme* s, const int64_t* secrets, uint64_t D,
+                              const int64_t* draws, uint64_t n_draws, int64_t* out, uint64_t out_cap) {
+    if (!h || !s) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL handle or scheme");
+    if ((D && !secrets) || (n_draws && !draws)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL input buffer");
+    HIP_TRY(hipSetDevice(h->device));
+    if (s->kind == SDA_SHARING_ADDITIVE) {
+        const uint64_t n = s->share_count;
+        if (n == 0) return fail(SDA_ERR_PRECONDITION, "share_count - 1 underflows (additive.rs:42)");
+        if (s->modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
+        if (n_draws != D * (n - 1))
+            return fail(SDA_ERR_INVALID_ARGUMENT, "expected %llu draws (dimension * (share_count - 1)), got %llu",
+                        (unsigned long long)(D * (n - 1)), (unsigned long long)n_draws);
+        if (out_cap < n * D) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
+        if (D == 0) return ok();
+        DevArena a;
+        if (sda_status st = stage(h, rup(D * 8) + rup(n_draws * 8) + rup(n * D * 8), &a)) return st;
+        int64_t* dsec = a.take<int64_t>(D);
+        int64_t* ddr = a.take<int64_t>(n_draws);
+        int64_t* dout = a.take<int64_t>(n * D);
+        HIP_TRY(hipMemcpyAsync(dsec, secrets, D * 8, hipMemcpyHostToDevice, h->stream));
+        if (n_draws) HIP_TRY(hipMemcpyAsync(ddr, draws, n_draws * 8, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(sda::launch_additive_generate(dsec, D, ddr, n, dout, s->modulus, h->stream));
+        HIP_TRY(hipMemcpyAsync(out, dout, n * D * 8, hipMemcpyDeviceToHost, h->stream));
+        return finish(h);
+    }
+    if (s->kind != SDA_SHARING_PACKED_SHAMIR) return fail(SDA_ERR_INVALID_ARGUMENT, "unknown sharing scheme kind");
+    if (sda_status st = check_packed(s)) return st;
+    const uint64_t k = s->secret_count, t = s->privacy_threshold, n = s->share_count;
+    const uint64_t B = (D + k - 1) / k;
+    if (n_draws != B * t)
+        return fail(SDA_ERR_INVALID_ARGUMENT, "expected %llu draws (batches * privacy_threshold), got %llu",
+                    (unsigned long long)(B * t), (unsigned long long)n_draws);
+    if (out_cap < n * B) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
+    if (B == 0) return ok();
+    DevArena a;
+    if (sda_status st = stage(h, rup(D * 8) + rup(n_draws * 8) + rup(n * B * 8), &a)) return st;
+    int64_t* dsec = a.take<int64_t>(D);
+    int64_t* ddr = a.take<int64_t>(n_draws);
+    int64_t* dout = a.take<int64_t>(n * B);
+    HIP_TRY(hipMemcpyAsync(dsec, secrets, D * 8, hipMemcpyHostToDevice, h->stream));
+    if (n_draws) HIP_TRY(hipMemcpyAsync(ddr, draws, n_draws * 8, hipMemcpyHostToDevice, h->stream));
+    sda::PackedGenArgs ga{dsec, D, 1, ddr, dout};
+    HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)k, (uint32_t)t, (uint32_t)n, (uint32_t)s->modulus,
+                                        (uint32_t)s->omega_secrets, (uint32_t)s->omega_shares, h->stream));
+    HIP_TRY(hipMemcpyAsync(out, dout, n * B * 8, hipMemcpyDeviceToHost, h->stream));
+    return finish(h);
+}
+
+// ---------------- ShareCombiner::combine ----------------
+static sda_status combine_rows(sda_engine* h, int64_t modulus, const int64_t* const* rows, const uint64_t* lens,
+                               uint64_t n_rows, int64_t* out, uint64_t out_cap, uint64_t* out_len,
+                               sda_status dim_err, const char* dim_msg) {
+    if (!h || (n_rows && (!rows || !lens)) || !out_len) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    HIP_TRY(hipSetDevice(h->device));
+    const uint64_t dim = n_rows ? lens[0] : 0;              // combiner.rs:17
+    *out_len = 0;
+    int64_t m;
+    for (uint64_t i = 0; i < n_rows; ++i)
+        if (lens[i] != dim) return fail(dim_err, "%s (row %llu has %llu elements, expected %llu)", dim_msg,
+                                        (unsigned long long)i, (unsigned long long)lens[i],
+                                        (unsigned long long)dim);
+    if (dim && n_rows) {
+        if (sda_status st = modulus_abs(modulus, &m)) return st;
+    } else {
+        m = 1;
+    }
+    if (out_cap < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
+    *out_len = dim;
+    if (dim == 0) return ok();
+    for (uint64_t i = 0; i < n_rows; ++i)
+        if (!rows[i]) return fail(SDA_ERR_INVALID_ARGUMENT, "row %llu is NULL", (unsigned long long)i);
+    DevArena a;
+    if (sda_status st = stage(h, rup(n_rows * dim * 8) + rup(dim * 8), &a)) return st;
+    int64_t* din = a.take<int64_t>(n_rows * dim);
+    int64_t* dout = a.take<int64_t>(dim);
+    if (sda_status st = upload_rows(h, din, rows, n_rows, dim)) return st;
+    HIP_TRY(sda::launch_combine_exact(din, n_rows, dim, dim, dout, m, h->stream));
+    HIP_TRY(hipMemcpyAsync(out, dout, dim * 8, hipMemcpyDeviceToHost, h->stream));
+    return finish(h);
+}
+
+sda_status sda_share_combine(sda_engine* h, const sda_sharing_scheme* s, const int64_t* const* rows,
+                             const uint64_t* lens, uint64_t n_rows, int64_t* out, uint64_t out_cap,
+                             uint64_t* out_len) {
+    if (!s) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL scheme");
+    // sharing/mod.rs:61-69: Additive -> modulus, PackedShamir -> prime_modulus (same field here)
+    return combine_rows(h, s->modulus, rows, lens, n_rows, out, out_cap, out_len, SDA_ERR_WRONG_DIMENSION,
+                        "Wrong dimension");
+}
+
+// ---------------- SecretReconstructor::reconstruct ----------------
+sda_status sda_secret_reconstruct(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,
+                                  const uint64_t* indices, const int64_t* const* rows, const uint64_t* lens,
+                                  uint64_t n_rows, int64_t* out, uint64_t out_cap, uint64_t* out_len) {
+    if (!h || !s || !out_len) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (s->kind == SDA_SHARING_ADDITIVE) {
+        // additive.rs:56-72: dimension = first row's length; indices are ignored
+        return combine_rows(h, s->modulus, rows, lens, n_rows, out, out_cap, out_len,
+                            SDA_ERR_MISMATCHING_DIMENSION, "Mismatching dimension");
+    }
+    if (s->kind != SDA_SHARING_PACKED_SHAMIR) return fail(SDA_ERR_INVALID_ARGUMENT, "unknown sharing scheme kind");
+    if (sda_status st = check_packed(s)) return st;
+    HIP_TRY(hipSetDevice(h->device));
+    const uint64_t k = s->secret_count;
+    const uint64_t B = (dimension + k - 1) / k;             // batched.rs:77
+    *out_len = 0;
+    if (out_cap < dimension) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
+    if (B == 0) { *out_len = 0; return ok(); }              // no batch => no error checks run
+    if (n_rows && (!rows || !lens || !indices)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    for (uint64_t i = 0; i < n_rows; ++i)                   // batched.rs:84 indexes [batch_index]
+        if (lens[i] < B) return fail(SDA_ERR_PRECONDITION, "index out of bounds: row %llu has %llu < %llu batches",
+                                     (unsigned long long)i, (unsigned long long)lens[i], (unsigned long long)B);
+    if (n_rows < s->privacy_threshold + k)                  // packed_shamir.rs:75
+        return fail(SDA_ERR_NOT_ENOUGH_SHARES, "Not enough shares to reconstruct (%llu < %llu)",
+                    (unsigned long long)n_rows, (unsigned long long)(s->privacy_threshold + k));
+    if (n_rows > 63) return fail(SDA_ERR_UNSUPPORTED, "more than 63 clerk shares per batch");
+    DevArena a;
+    const size_t tab = sda::packed_reveal_scratch_bytes((uint32_t)n_rows, (uint32_t)k);
+    if (sda_status st = stage(h, rup(n_rows * B * 8) + rup(dimension * 8) + rup(tab), &a)) return st;
+    int64_t* din = a.take<int64_t>(n_rows * B);
+    int64_t* dout = a.take<int64_t>(dimension);
+    int64_t* dtab = a.take<int64_t>(tab / 8 + 1);
+    for (uint64_t i = 0; i < n_rows; ++i)
+        HIP_TRY(hipMemcpyAsync(din + i * B, rows[i], B * 8, hipMemcpyHostToDevice, h->stream));
+    sda::PackedRevealArgs ra{din, dimension, 1, dout};
+    HIP_TRY(sda::launch_packed_reveal(ra, indices, (uint32_t)n_rows, (uint32_t)k, (uint32_t)s->privacy_threshold,
+                                      (uint32_t)s->share_count, (uint32_t)s->modulus, (uint32_t)s->omega_secrets,
+                                      (uint32_t)s->omega_shares, SDA_REVEAL_EXACT, dtab, h->stream));
+    HIP_TRY(hipMemcpyAsync(out, dout, dimension * 8, hipMemcpyDeviceToHost, h->stream));
+    *out_len = dimension;
+    return finish(h);
+}
+
+// ---------------- masking ----------------
+sda_status sda_secret_mask(sda_engine* h, const sda_masking_scheme* s, const int64_t* secrets, uint64_t D,
+                           const uint32_t* seed, uint64_t seed_words, const int64_t* full_masks, int64_t* mask_out,
+                           uint64_t mask_cap, uint64_t* mask_len, int64_t* masked_out) {
+    if (!h || !s || !mask_len || (D && (!secrets || !masked_out)))
+        return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    HIP_TRY(hipSetDevice(h->device));
+    *mask_len = 0;
+    if (s->kind == SDA_MASKING_NONE) {                      // none.rs:14-19
+        if (D) memcpy(masked_out, secrets, D * 8);
+        return ok();
+    }
+    if (s->modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
+    if (s->kind == SDA_MASKING_FULL) {                      // full.rs:22-35
+        if (D && !full_masks) return fail(SDA_ERR_INVALID_ARGUMENT, "Full masking needs the drawn masks");
+        if (mask_cap < D) return fail(SDA_ERR_INVALID_ARGUMENT, "mask buffer too small");
+        if (D == 0) return ok();
+        DevArena a;
+        if (sda_status st = stage(h, 3 * rup(D * 8), &a)) return st;
+        int64_t* ds = a.take<int64_t>(D);
+        int64_t* dm = a.take<int64_t>(D);
+        int64_t* dout = a.take<int64_t>(D);
+        HIP_TRY(hipMemcpyAsync(ds, secrets, D * 8, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(dm, full_masks, D * 8, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(sda::launch_addsub_trem(ds, dm, +1, D, dout, s->modulus, h->stream));
+        HIP_TRY(hipMemcpyAsync(masked_out, dout, D * 8, hipMemcpyDeviceToHost, h->stream));
+        memcpy(mask_out, full_masks, D * 8);
+        *mask_len = D;
+        return finish(h);
+    }
+    if (s->kind != SDA_MASKING_CHACHA) return fail(SDA_ERR_INVALID_ARGUMENT, "unknown masking scheme kind");
+    // chacha.rs:26 assert_eq!(self.dimension, secrets.len())
+    if (s->dimension != D) return fail(SDA_ERR_PRECONDITION, "assertion failed: dimension == secrets.len()");
+    const uint64_t want_words = (s->seed_bitsize + 31) / 32;   // chacha.rs:30
+    if (seed_words != want_words || (seed_words && !seed))
+        return fail(SDA_ERR_PRECONDITION, "expected %llu seed words for seed_bitsize %llu",
+                    (unsigned long long)want_words, (unsigned long long)s->seed_bitsize);
+    if (mask_cap < seed_words) return fail(SDA_ERR_INVALID_ARGUMENT, "mask buffer too small");
+    for (uint64_t i = 0; i < seed_words; ++i) mask_out[i] = (int64_t)seed[i];   // chacha.rs:48-50
+    *mask_len = seed_words;
+    if (D == 0) return ok();
+    const uint32_t w = (uint32_t)(seed_words < 8 ? seed_words : 8);           // key holds 8 words
+    if (sda_status st = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D) + 64 + D * 8)) return st;
+    DevArena a;
+    if (sda_status st = stage(h, 2 * rup(D * 8), &a)) return st;
+    int64_t* ds = a.take<int64_t>(D);
+    int64_t* dout = a.take<int64_t>(D);
+    HIP_TRY(hipMemcpyAsync(ds, secrets, D * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(sda::launch_chacha_mask(s->modulus, seed, w, ds, D, dout, h->work, h->stream));
+    HIP_TRY(hipMemcpyAsync(masked_out, dout, D * 8, hipMemcpyDeviceToHost, h->stream));
+    return finish(h);
+}
+
+sda_status sda_mask_combine(sda_engine* h, const sda_masking_scheme* s, const int64_t* const* rows,
+                            const uint64_t* lens, uint64_t n_rows, int64_t* out, uint64_t out_cap,
+                            uint64_t* out_len) {
+    if (!h || !s || !out_len || (n_rows && (!rows || !lens))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    *out_len = 0;
+    if (s->kind == SDA_MASKING_NONE) {                      // none.rs:22-25
+        for (uint64_t i = 0; i < n_rows; ++i)
+            if (lens[i]) return fail(SDA_ERR_PRECONDITION, "assertion failed: masks.iter().all(|mask| mask.len() == 0)");
+        return ok();
+    }
+    if (s->kind == SDA_MASKING_FULL) {                      // full.rs:38-50 (panics on mismatch)
+        const uint64_t dim = n_rows ? lens[0] : 0;
+        for (uint64_t i = 0; i < n_rows; ++i)
+            if (lens[i] != dim) return fail(SDA_ERR_PRECONDITION, "assertion failed: mask.len() == dimension");
+        return combine_rows(h, s->modulus, rows, lens, n_rows, out, out_cap, out_len, SDA_ERR_PRECONDITION,
+                            "assertion failed");
+    }
+    if (s->kind != SDA_MASKING_CHACHA) return fail(SDA_ERR_INVALID_ARGUMENT, "unknown masking scheme kind");
+    HIP_TRY(hipSetDevice(h->device));
+    const uint64_t D = s->dimension;                        // chacha.rs:58 vec![0; self.dimension]
+    if (out_cap < D) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
+    if (D && s->modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
+    uint64_t w = 0;
+    for (uint64_t i = 0; i < n_rows; ++i) w = lens[i] > w ? lens[i] : w;
+    if (w > 8) w = 8;                                       // ChaChaRng key = first 8 seed words
+    if (w == 0) w = 1;                                      // empty seeds == all-zero key
+    std::vector<uint32_t> seeds(n_rows * w, 0u);            // shorter seeds pad with zero key words
+    for (uint64_t i = 0; i < n_rows; ++i)
+        for (uint64_t j = 0; j < lens[i] && j < w; ++j) seeds[i * w + j] = (uint32_t)rows[i][j];   // chacha.rs:62-64
+    *out_len = D;
+    if (D == 0) return ok();
+    if (sda_status st = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D))) return st;
+    DevArena a;
+    if (sda_status st = stage(h, rup(seeds.size() * 4 + 4) + rup(D * 8), &a)) return st;
+    uint32_t* dseeds = a.take<uint32_t>(seeds.size() + 1);
+    int64_t* dout = a.take<int64_t>(D);
+    if (!seeds.empty())
+        HIP_TRY(hipMemcpyAsync(dseeds, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, h->stream));
+    int fixups = 0;
+    HIP_TRY(sda::launch_chacha_mask_combine(s->modulus, D, dseeds, (uint32_t)w, n_rows, dout, h->work, h->stream,
+                                            &fixups));
+    HIP_TRY(hipMemcpyAsync(out, dout, D * 8, hipMemcpyDeviceToHost, h->stream));
+    return finish(h);
+}
+
+sda_status sda_secret_unmask(sda_engine* h, const sda_masking_scheme* s, const int64_t* mask, uint64_t mask_len,
+                             const int64_t* masked, uint64_t masked_len, int64_t* out, uint64_t out_cap,
+                             uint64_t* out_len) {
+    if (!h || !s || !out_len || (masked_len && (!masked || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    *out_len = 0;
+    if (out_cap < masked_len) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
+    if (s->kind == SDA_MASKING_NONE) {                      // none.rs:28-32
+        if (mask_len != 0) return fail(SDA_ERR_PRECONDITION, "assertion failed: values.0.len() == 0");
+        if (masked_len) memcpy(out, masked, masked_len * 8);
+        *out_len = masked_len;
+        return ok();
+    }
+    if (s->kind != SDA_MASKING_FULL && s->kind != SDA_MASKING_CHACHA)
+        return fail(SDA_ERR_INVALID_ARGUMENT, "unknown masking scheme kind");
+    if (mask_len != masked_len) return fail(SDA_ERR_PRECONDITION, "assertion failed: mask.len() == masked_secrets.len()");
+    *out_len = masked_len;
+    if (masked_len == 0) return ok();
+    int64_t m;
+    if (sda_status st = modulus_abs(s->modulus, &m)) return st;
+    HIP_TRY(hipSetDevice(h->device));
+    const uint64_t D = masked_len;
+    DevArena a;
+    if (sda_status st = stage(h, 3 * rup(D * 8), &a)) return st;
+    int64_t* dm = a.take<int64_t>(D);
+    int64_t* dms = a.take<int64_t>(D);
+    int64_t* dout = a.take<int64_t>(D);
+    HIP_TRY(hipMemcpyAsync(dm, mask, D * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(dms, masked, D * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(sda::launch_addsub_trem(dms, dm, -1, D, dout, m, h->stream));      // (ms - m) % q
+    HIP_TRY(hipMemcpyAsync(out, dout, D * 8, hipMemcpyDeviceToHost, h->stream));
+    return finish(h);
+}
+
+sda_status sda_recipient_positive(sda_engine* h, int64_t modulus, const int64_t* values, uint64_t n, int64_t* out) {
+    if (!h || (n && (!values || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (n == 0) return ok();
+    HIP_TRY(hipSetDevice(h->device));
+    DevArena a;
+    if (sda_status st = stage(h, 2 * rup(n * 8), &a)) return st;
+    int64_t* dv = a.take<int64_t>(n);
+    int64_t* dout = a.take<int64_t>(n);
+    HIP_TRY(hipMemcpyAsync(dv, values, n * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(sda::launch_positive(dv, n, dout, modulus, h->stream));
+    HIP_TRY(hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, h->stream));
+    return finish(h);
+}
+
+// ---------------- device-resident entry points ----------------
+sda_status sda_combine_dev(sda_engine* h, int64_t modulus, const int64_t* shares, uint64_t n, uint64_t dim,
+                           uint64_t row_stride, int64_t* out, void* stream) {
+    if (!h || (dim && (!out || (n && !shares)))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (n > 1 && row_stride < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "row_stride < dim");
+    int64_t m;
+    if (sda_status st = modulus_abs(modulus, &m)) return st;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(sda::launch_combine_exact(shares, n, dim, n > 1 ? row_stride : dim, out, m, pick(h, stream)));
+    return ok();
+}
+
+sda_status sda_combine_finalize_dev(sda_engine* h, int64_t modulus, const int64_t* sums, uint64_t dim, int64_t* out,
+                                    void* stream) {
+    if (!h || (dim && (!sums || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    int64_t m;
+    if (sda_status st = modulus_abs(modulus, &m)) return st;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(sda::launch_mod_canonical(sums, dim, out, m, pick(h, stream)));
+    return ok();
+}
+
+sda_status sda_packed_generate_dev(sda_engine* h, const sda_sharing_scheme* s, const int64_t* secrets,
+                                   uint64_t dimension, uint64_t n_vectors, const int64_t* draws, int64_t* out,
+                                   void* stream) {
+    if (!h || !s || s->kind != SDA_SHARING_PACKED_SHAMIR) return fail(SDA_ERR_INVALID_ARGUMENT, "need a PackedShamir scheme");
+    if (sda_status st = check_packed(s)) return st;
+    if (n_vectors > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 vectors per launch");
+    HIP_TRY(hipSetDevice(h->device));
+    sda::PackedGenArgs ga{secrets, dimension, n_vectors, draws, out};
+    HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)s->secret_count, (uint32_t)s->privacy_threshold,
+                                        (uint32_t)s->share_count, (uint32_t)s->modulus, (uint32_t)s->omega_secrets,
+                                        (uint32_t)s->omega_shares, pick(h, stream)));
+    return ok();
+}
+
+sda_status sda_packed_reconstruct_dev(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,
+                                      const uint64_t* indices, uint64_t n_idx, uint64_t n_vectors,
+                                      const int64_t* shares, int64_t* out, int32_t mode, void* stream) {
+    if (!h || !s || s->kind != SDA_SHARING_PACKED_SHAMIR) return fail(SDA_ERR_INVALID_ARGUMENT, "need a PackedShamir scheme");
+    if (sda_status st = check_packed(s)) return st;
+    if (mode != SDA_REVEAL_EXACT && mode != SDA_REVEAL_CANONICAL) return fail(SDA_ERR_INVALID_ARGUMENT, "bad mode");
+    if (n_idx < s->privacy_threshold + s->secret_count)
+        return fail(SDA_ERR_NOT_ENOUGH_SHARES, "Not enough shares to reconstruct");
+    if (n_idx > 63) return fail(SDA_ERR_UNSUPPORTED, "more than 63 clerk shares per batch");
+    if (n_vectors > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 vectors per launch");
+    HIP_TRY(hipSetDevice(h->device));
+    const size_t tab = sda::packed_reveal_scratch_bytes((uint32_t)n_idx, (uint32_t)s->secret_count);
+    if (sda_status st = ensure(&h->work, &h->work_bytes, tab)) return st;
+    sda::PackedRevealArgs ra{shares, dimension, n_vectors, out};
+    hipError_t e = sda::launch_packed_reveal(ra, indices, (uint32_t)n_idx, (uint32_t)s->secret_count,
+                                             (uint32_t)s->privacy_threshold, (uint32_t)s->share_count,
+                                             (uint32_t)s->modulus, (uint32_t)s->omega_secrets,
+                                             (uint32_t)s->omega_shares, mode, (int64_t*)h->work, pick(h, stream));
+    if (e == hipErrorInvalidValue && mode == SDA_REVEAL_CANONICAL)
+        return fail(SDA_ERR_UNSUPPORTED, "canonical reveal needs distinct clerk indices");
+    HIP_TRY(e);
+    return ok();
+}
+
+sda_status sda_additive_generate_dev(sda_engine* h, int64_t modulus, uint64_t share_count, const int64_t* secrets,
+                                     uint64_t dimension, const int64_t* draws, int64_t* out, void* stream) {
+    if (!h) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL handle");
+    if (share_count == 0) return fail(SDA_ERR_PRECONDITION, "share_count - 1 underflows (additive.rs:42)");
+    if (modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(sda::launch_additive_generate(secrets, dimension, draws, share_count, out, modulus, pick(h, stream)));
+    return ok();
+}
+
+sda_status sda_chacha_mask_combine_dev(sda_engine* h, int64_t modulus, uint64_t dimension, const uint32_t* seeds,
+                                       uint64_t w, uint64_t n_seeds, int64_t* out, void* stream) {
+    if (!h || (dimension && !out) || (n_seeds && w && !seeds)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (dimension && modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
+    if (w == 0 || w > 8) return fail(SDA_ERR_INVALID_ARGUMENT, "seed width must be 1..8 words");
+    HIP_TRY(hipSetDevice(h->device));
+    if (sda_status st = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(dimension))) return st;
+    int fixups = 0;
+    HIP_TRY(sda::launch_chacha_mask_combine(modulus, dimension, seeds, (uint32_t)w, n_seeds, out, h->work,
+                                            pick(h, stream), &fixups));
+    return ok();
+}
+
+sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64_t cols, uint64_t seed, int64_t lo,
+                              int64_t hi, void* stream) {
+    if (!h || (rows * cols && !dst)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (hi <= lo) return fail(SDA_ERR_INVALID_ARGUMENT, "need hi > lo");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(sda::launch_synth_fill(dst, rows, cols, seed, lo, hi, pick(h, stream)));
+    return ok();
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// kernels.h -- internal launchers (not part of the C ABI).  Each returns hipSuccess or the
+// launch error; all of them only enqueue on `stream`.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "modarith.h"
+
+namespace sda {
+
+// ---- combine.hip ----
+// Exact clerk combine: out[j] = fold over rows of (r + v) % m  (combiner.rs:22-25).
+hipError_t launch_combine_exact(const int64_t* in, uint64_t n, uint64_t dim, uint64_t stride,
+                                int64_t* out, int64_t modulus, hipStream_t s);
+// Canonical residue of u64 sums (multi-GPU finalize).
+hipError_t launch_mod_canonical(const int64_t* sums, uint64_t dim, int64_t* out, int64_t modulus,
+                                hipStream_t s);
+
+// ---- elementwise.hip ----
+hipError_t launch_additive_generate(const int64_t* secrets, uint64_t D, const int64_t* draws,
+                                    uint64_t n, int64_t* out, int64_t modulus, hipStream_t s);
+// out[i] = (a[i] + sign * b[i]) % m   (sign = +1: mask, -1: unmask)
+hipError_t launch_addsub_trem(const int64_t* a, const int64_t* b, int sign, uint64_t D,
+                              int64_t* out, int64_t modulus, hipStream_t s);
+hipError_t launch_positive(const int64_t* v, uint64_t D, int64_t* out, int64_t modulus,
+                           hipStream_t s);
+hipError_t launch_synth_fill(int64_t* dst, uint64_t rows, uint64_t cols, uint64_t seed,
+                             int64_t lo, int64_t hi, hipStream_t s);
+
+// ---- packed_shamir.hip ----
+struct PackedPlan;   // defined in packed_shamir.hip (twiddles, Montgomery constants)
+struct PackedGenArgs {
+    const int64_t* secrets; uint64_t dimension; uint64_t n_vectors;
+    const int64_t* draws; int64_t* out;
+};
+hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t, uint32_t n,
+                                  uint32_t p, uint32_t omega_secrets, uint32_t omega_shares,
+                                  hipStream_t s);
+struct PackedRevealArgs {
+    const int64_t* shares; uint64_t dimension; uint64_t n_vectors; int64_t* out;
+};
+hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indices, uint32_t n_idx,
+                                uint32_t k, uint32_t t, uint32_t n, uint32_t p,
+                                uint32_t omega_secrets, uint32_t omega_shares, int mode,
+                                int64_t* scratch_dev, hipStream_t s);
+size_t packed_reveal_scratch_bytes(uint32_t n_idx, uint32_t k);
+
+// ---- chacha.hip ----
+// Combine of n_seeds ChaCha mask streams (chacha.rs:57-76).  `work` must hold
+// chacha_work_bytes(...) bytes of device memory.
+size_t chacha_work_bytes(uint64_t n_seeds);
+hipError_t launch_chacha_mask_combine(int64_t modulus, uint64_t dimension, const uint32_t* seeds,
+                                      uint32_t w, uint64_t n_seeds, int64_t* out, void* work,
+                                      hipStream_t s, int* fixups_out);
+// masked[i] = (secrets[i] + gen_range_i) % m for one seed (chacha.rs:36-45)
+hipError_t launch_chacha_mask(int64_t modulus, const uint32_t* seed_host, uint32_t w,
+                              const int64_t* secrets, uint64_t D, int64_t* masked, void* work,
+                              hipStream_t s);
+
+}  // namespace sda

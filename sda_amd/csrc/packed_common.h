@@ -1,0 +1,129 @@
+#pragma once
+// packed_common.h -- shared by packed_gen.hip / packed_reveal.hip: north-star kernel (2): packed-Shamir share generation and reveal.
+//
+// Reference call sites: client/src/crypto/sharing/packed_shamir.rs:40-43 (share) and :73-77
+// (reconstruct), batched by client/src/crypto/sharing/batched.rs:19-53 / :69-97.  The
+// arithmetic lives in threshold-secret-sharing 0.2 (absent from the reference tree):
+//   share:       values = [0, secrets(k), randomness(t)]  (length L = k+t+1, a power of 2)
+//                coeffs = fft2_inverse(values, omega_secrets)   recursive radix-2, `%` per op
+//                points = fft3(coeffs ++ zeros, omega_shares)    recursive radix-3 over n+1
+//                shares = points[1..=n]
+//   reconstruct: Newton divided differences through (1,0) and (omega_shares^(i+1), share_i),
+//                evaluated at omega_secrets^e, e = 1..k.
+// Every intermediate is an i64 in (-p, p) whose SIGN depends on the exact operation order
+// (Rust's truncated `%`).  The kernels reproduce them bit for bit: for each `(expr) % p` they
+// compute (i) the canonical residue with 32-bit Montgomery products (R = 2^32, no 64-bit
+// division) and (ii) the sign of the exact i64 expr with one 32x32->64 multiply-add, then
+// recombine (trunc_from).  No MFMA: this is not a dense contraction (north star).
+//
+// One lane = one batch.  The in-place DIT on bit/digit-reversed registers performs exactly the
+// butterflies of tss' recursion (same operands, same twiddles, same `%` points).  Batches whose
+// inputs fall outside (-p, p) (raw i64 secrets / shares) take a generic exact path that mirrors
+// the recursion with wrapping i64 arithmetic.
+//
+// Reveal comes in two modes: EXACT (Newton, tss' signed representatives; VALU-bound) and
+// CANONICAL (Lagrange weights for the clerk-index set, residues in [0, p); HBM-bound), equal
+// mod p and equal after RecipientOutput::positive (receive.rs:14-20).
+#include <string.h>
+
+#include <vector>
+
+#include "kernels.h"
+
+namespace sda {
+namespace packed {
+
+// ------------------------------------------------------------------------------------------
+// host-side exact helpers (tss numtheory semantics: truncated `%`)
+// ------------------------------------------------------------------------------------------
+inline int64_t h_rem(int64_t a, int64_t p) { return a % p; }
+inline int64_t h_powmod(int64_t x, uint32_t e, int64_t p) {      // numtheory::mod_pow
+    int64_t acc = 1;
+    while (e > 0) {
+        if (e & 1u) acc = h_rem((int64_t)((uint64_t)acc * (uint64_t)x), p);
+        x = h_rem((int64_t)((uint64_t)x * (uint64_t)x), p);
+        e >>= 1;
+    }
+    return acc;
+}
+inline void h_egcd(int64_t a, int64_t b, int64_t* s, int64_t* t) {     // numtheory::gcd
+    if (b == 0) { *s = 1; *t = 0; return; }
+    int64_t n = a / b, c = a % b, s1, t1;
+    h_egcd(b, c, &s1, &t1);
+    *s = t1; *t = s1 - t1 * n;
+}
+inline int64_t h_modinv(int64_t k, int64_t p) {                 // numtheory::mod_inverse
+    int64_t k2 = k % p, s, t, r;
+    if (k2 < 0) { h_egcd(p, -k2, &s, &t); r = -t; } else { h_egcd(p, k2, &s, &t); r = t; }
+    return (p + r) % p;
+}
+inline uint32_t to_mont(int64_t x, int64_t p) {            // canonical x -> x R mod p
+    int64_t c = x % p; if (c < 0) c += p;
+    return (uint32_t)((((unsigned __int128)c) << 32) % (uint64_t)p);
+}
+
+// ------------------------------------------------------------------------------------------
+// generation tables (kernel argument, uniform => scalar loads)
+// ------------------------------------------------------------------------------------------
+struct GenTables {
+    MontP M;
+    uint32_t linv, linv_m;          // L^{-1} mod p (canonical, Montgomery)
+    uint32_t tw2[64], tw2_m[64];    // radix-2 level len: entries [len/2 - 1, len - 1)
+    uint32_t tw3[120], tw3_m[120];  // radix-3 level len: entries [(len-3)/2, (len-3)/2 + len)
+    uint32_t sq3[120], sq3_m[120];  // x^2 % p per radix-3 entry
+};
+
+inline GenTables make_gen_tables(uint32_t L, uint32_t N3, int64_t p, int64_t ws, int64_t wn) {
+    GenTables T;
+    memset(&T, 0, sizeof(T));
+    T.M = make_mont((uint32_t)p);
+    // fft2_inverse: fft2 over omega^-1; recursion squares omega at each level (mod_pow(ω, 2))
+    const int64_t winv = h_modinv(ws, p);
+    T.linv = (uint32_t)h_modinv((int64_t)L, p);
+    T.linv_m = to_mont(T.linv, p);
+    {
+        int64_t om = winv;                 // omega for the top level (len = L)
+        std::vector<int64_t> per_level;    // omega per level, top first
+        for (uint32_t len = L; len >= 2; len /= 2) { per_level.push_back(om); om = h_powmod(om, 2, p); }
+        int lvl = (int)per_level.size() - 1;
+        for (uint32_t len = 2; len <= L; len *= 2, --lvl) {
+            for (uint32_t i = 0; i < len / 2; ++i) {
+                const int64_t w = h_powmod(per_level[lvl], i, p);
+                T.tw2[len / 2 - 1 + i] = (uint32_t)w;
+                T.tw2_m[len / 2 - 1 + i] = to_mont(w, p);
+            }
+        }
+    }
+    {
+        int64_t om = wn;
+        std::vector<int64_t> per_level;
+        for (uint32_t len = N3; len >= 3; len /= 3) { per_level.push_back(om); om = h_powmod(om, 3, p); }
+        int lvl = (int)per_level.size() - 1;
+        for (uint32_t len = 3; len <= N3; len *= 3, --lvl) {
+            for (uint32_t j = 0; j < len; ++j) {
+                const int64_t x = h_powmod(per_level[lvl], j, p);
+                const int64_t x2 = h_rem(x * x, p);
+                const uint32_t o = (len - 3) / 2 + j;
+                T.tw3[o] = (uint32_t)x; T.tw3_m[o] = to_mont(x, p);
+                T.sq3[o] = (uint32_t)x2; T.sq3_m[o] = to_mont(x2, p);
+            }
+        }
+    }
+    return T;
+}
+
+
+constexpr int ilog(int x, int b) { return x <= 1 ? 0 : 1 + ilog(x / b, b); }
+constexpr int ipow(int b, int e) { return e == 0 ? 1 : b * ipow(b, e - 1); }
+constexpr int rev_digits(int i, int base, int ndig) {
+    int r = 0;
+    for (int d = 0; d < ndig; ++d) { r = r * base + i % base; i /= base; }
+    return r;
+}
+
+__device__ __forceinline__ int64_t wmul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+__device__ __forceinline__ int64_t wadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+__device__ __forceinline__ int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+
+}  // namespace packed
+}  // namespace sda

@@ -1,0 +1,258 @@
+"""ctypes binding of libsda_engine.so (include/sda_engine.h).
+
+This is the Python-side consumer of the C ABI: the parity tests and bench.py call the MI355X
+engine only through it.  There is deliberately no CPU fallback: if the shared library is
+missing or a call fails, an exception is raised.
+
+Trait mirrors (reference: client/src/crypto/{sharing,masking}/mod.rs):
+    share_generate     ShareGenerator::generate        (sharing/mod.rs:14-17)
+    share_combine      ShareCombiner::combine          (sharing/mod.rs:23-25)
+    secret_reconstruct SecretReconstructor::reconstruct (sharing/mod.rs:31-33)
+    secret_mask        SecretMasker::mask              (masking/mod.rs:13-15)
+    mask_combine       MaskCombiner::combine           (masking/mod.rs:21-23)
+    secret_unmask      SecretUnmasker::unmask          (masking/mod.rs:29-31)
+    positive           RecipientOutput::positive       (receive.rs:14-20)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import schemes as S
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsda_engine.so")
+
+OK = 0
+ERR_BATCH_INPUT_WRONG_LENGTH = 1
+ERR_PACKED_SHARING_FAILED = 2
+ERR_WRONG_DIMENSION = 3
+ERR_MISMATCHING_DIMENSION = 4
+ERR_INPUTS_MUST_HAVE_SAME_LENGTH = 5
+ERR_NOT_ENOUGH_SHARES = 6
+ERR_PRECONDITION = 64
+ERR_INVALID_ARGUMENT = 65
+ERR_UNSUPPORTED = 66
+ERR_DEVICE = 67
+ERR_OUT_OF_MEMORY = 68
+
+REVEAL_EXACT = 0
+REVEAL_CANONICAL = 1
+
+_i64p = C.POINTER(C.c_int64)
+_u64p = C.POINTER(C.c_uint64)
+_u32p = C.POINTER(C.c_uint32)
+_vp = C.c_void_p
+_st = C.c_int
+
+# (name, restype, argtypes) for every symbol declared in include/sda_engine.h
+SIGNATURES = [
+    ("sda_abi_version", C.c_int, []),
+    ("sda_engine_create", _st, [C.c_int, C.POINTER(_vp)]),
+    ("sda_engine_destroy", None, [_vp]),
+    ("sda_engine_synchronize", _st, [_vp]),
+    ("sda_last_error_message", C.c_char_p, []),
+    ("sda_status_string", C.c_char_p, [C.c_int]),
+    ("sda_scheme_input_size", C.c_uint64, [C.POINTER(S.SharingSchemeC)]),
+    ("sda_scheme_output_size", C.c_uint64, [C.POINTER(S.SharingSchemeC)]),
+    ("sda_scheme_privacy_threshold", C.c_uint64, [C.POINTER(S.SharingSchemeC)]),
+    ("sda_scheme_reconstruction_threshold", C.c_uint64, [C.POINTER(S.SharingSchemeC)]),
+    ("sda_share_length", C.c_uint64, [C.POINTER(S.SharingSchemeC), C.c_uint64]),
+    ("sda_share_generate", _st, [_vp, C.POINTER(S.SharingSchemeC), _i64p, C.c_uint64, _i64p, C.c_uint64,
+                                 _i64p, C.c_uint64]),
+    ("sda_share_combine", _st, [_vp, C.POINTER(S.SharingSchemeC), C.POINTER(_i64p), _u64p, C.c_uint64,
+                                _i64p, C.c_uint64, _u64p]),
+    ("sda_secret_reconstruct", _st, [_vp, C.POINTER(S.SharingSchemeC), C.c_uint64, _u64p, C.POINTER(_i64p),
+                                     _u64p, C.c_uint64, _i64p, C.c_uint64, _u64p]),
+    ("sda_secret_mask", _st, [_vp, C.POINTER(S.MaskingSchemeC), _i64p, C.c_uint64, _u32p, C.c_uint64, _i64p,
+                              _i64p, C.c_uint64, _u64p, _i64p]),
+    ("sda_mask_combine", _st, [_vp, C.POINTER(S.MaskingSchemeC), C.POINTER(_i64p), _u64p, C.c_uint64, _i64p,
+                               C.c_uint64, _u64p]),
+    ("sda_secret_unmask", _st, [_vp, C.POINTER(S.MaskingSchemeC), _i64p, C.c_uint64, _i64p, C.c_uint64, _i64p,
+                                C.c_uint64, _u64p]),
+    ("sda_recipient_positive", _st, [_vp, C.c_int64, _i64p, C.c_uint64, _i64p]),
+    ("sda_combine_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp, _vp]),
+    ("sda_combine_finalize_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, _vp, _vp]),
+    ("sda_packed_generate_dev", _st, [_vp, C.POINTER(S.SharingSchemeC), _vp, C.c_uint64, C.c_uint64, _vp, _vp,
+                                      _vp]),
+    ("sda_packed_reconstruct_dev", _st, [_vp, C.POINTER(S.SharingSchemeC), C.c_uint64, _u64p, C.c_uint64,
+                                         C.c_uint64, _vp, _vp, C.c_int32, _vp]),
+    ("sda_additive_generate_dev", _st, [_vp, C.c_int64, C.c_uint64, _vp, C.c_uint64, _vp, _vp, _vp]),
+    ("sda_chacha_mask_combine_dev", _st, [_vp, C.c_int64, C.c_uint64, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
+    ("sda_synth_fill_dev", _st, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int64, C.c_int64, _vp]),
+]
+
+_lib = None
+
+
+def load_library():
+    """Load the in-tree engine library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"MI355X engine not built: {LIB_PATH} is missing (run `make` / __graft_entry__.build())")
+        lib = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+class SdaError(Exception):
+    """A non-OK sda_status.  `.status` is the code; for 1..6 str(e) starts with the reference's string."""
+
+    def __init__(self, status: int, message: str):
+        self.status = status
+        super().__init__(message)
+
+
+def _check(st: int):
+    if st != OK:
+        lib = load_library()
+        detail = lib.sda_last_error_message().decode()
+        base = lib.sda_status_string(st).decode()
+        raise SdaError(st, f"{base}: {detail}" if detail and detail != base else base)
+
+
+def _arr(a, dtype=np.int64):
+    return np.ascontiguousarray(np.asarray(a, dtype=dtype))
+
+
+def _ptr(a, t=_i64p):
+    return a.ctypes.data_as(t)
+
+
+def _rows(rows):
+    arrs = [_arr(r) for r in rows]
+    n = len(arrs)
+    ptrs = (_i64p * max(n, 1))(*[_ptr(a) for a in arrs])
+    lens = (C.c_uint64 * max(n, 1))(*[a.size for a in arrs])
+    return arrs, ptrs, lens, n
+
+
+class Engine:
+    """One engine handle = one HIP device + one stream (sda_engine_create)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = _vp()
+        _check(self.lib.sda_engine_create(device, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.sda_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------- trait mirrors ----------------
+    def share_generate(self, scheme, secrets, draws) -> np.ndarray:
+        s = scheme.c()
+        sec = _arr(secrets)
+        dr = _arr(draws).reshape(-1)
+        B = self.lib.sda_share_length(C.byref(s), sec.size)
+        n = scheme.output_size()
+        out = np.zeros(max(n * B, 1), np.int64)
+        _check(self.lib.sda_share_generate(self.h, C.byref(s), _ptr(sec), sec.size, _ptr(dr), dr.size, _ptr(out),
+                                           out.size))
+        return out[: n * B].reshape(n, B)
+
+    def share_combine(self, scheme, rows: Sequence) -> np.ndarray:
+        s = scheme.c()
+        arrs, ptrs, lens, n = _rows(rows)
+        cap = arrs[0].size if arrs else 0
+        out = np.zeros(max(cap, 1), np.int64)
+        olen = C.c_uint64(0)
+        _check(self.lib.sda_share_combine(self.h, C.byref(s), ptrs, lens, n, _ptr(out), out.size, C.byref(olen)))
+        return out[: olen.value]
+
+    def secret_reconstruct(self, scheme, dimension: int, indexed_shares) -> np.ndarray:
+        s = scheme.c()
+        idx = _arr([i for i, _ in indexed_shares], np.uint64)
+        arrs, ptrs, lens, n = _rows([r for _, r in indexed_shares])
+        cap = max(dimension, arrs[0].size if arrs else 0, 1)
+        out = np.zeros(cap, np.int64)
+        olen = C.c_uint64(0)
+        _check(self.lib.sda_secret_reconstruct(self.h, C.byref(s), dimension, _ptr(idx, _u64p), ptrs, lens, n,
+                                               _ptr(out), out.size, C.byref(olen)))
+        return out[: olen.value]
+
+    def secret_mask(self, scheme, secrets, seed: Optional[Sequence[int]] = None, full_masks=None):
+        s = scheme.c()
+        sec = _arr(secrets)
+        sd = _arr(seed if seed is not None else [], np.uint32)
+        fm = _arr(full_masks) if full_masks is not None else None
+        mask = np.zeros(max(sec.size, sd.size, 1), np.int64)
+        masked = np.zeros(max(sec.size, 1), np.int64)
+        mlen = C.c_uint64(0)
+        _check(self.lib.sda_secret_mask(self.h, C.byref(s), _ptr(sec), sec.size, _ptr(sd, _u32p), sd.size,
+                                        _ptr(fm) if fm is not None else None, _ptr(mask), mask.size,
+                                        C.byref(mlen), _ptr(masked)))
+        return mask[: mlen.value], masked[: sec.size]
+
+    def mask_combine(self, scheme, rows: Sequence) -> np.ndarray:
+        s = scheme.c()
+        arrs, ptrs, lens, n = _rows(rows)
+        cap = max(getattr(scheme, "dimension", 0), arrs[0].size if arrs else 0, 1)
+        out = np.zeros(cap, np.int64)
+        olen = C.c_uint64(0)
+        _check(self.lib.sda_mask_combine(self.h, C.byref(s), ptrs, lens, n, _ptr(out), out.size, C.byref(olen)))
+        return out[: olen.value]
+
+    def secret_unmask(self, scheme, values) -> np.ndarray:
+        s = scheme.c()
+        mask, masked = _arr(values[0]), _arr(values[1])
+        out = np.zeros(max(masked.size, 1), np.int64)
+        olen = C.c_uint64(0)
+        _check(self.lib.sda_secret_unmask(self.h, C.byref(s), _ptr(mask), mask.size, _ptr(masked), masked.size,
+                                          _ptr(out), out.size, C.byref(olen)))
+        return out[: olen.value]
+
+    def positive(self, modulus: int, values) -> np.ndarray:
+        v = _arr(values)
+        out = np.zeros(max(v.size, 1), np.int64)
+        _check(self.lib.sda_recipient_positive(self.h, modulus, _ptr(v), v.size, _ptr(out)))
+        return out[: v.size]
+
+    def synchronize(self):
+        _check(self.lib.sda_engine_synchronize(self.h))
+
+    # ---------------- device-resident entry points (raw device pointers, hipStream_t) ----------------
+    def combine_dev(self, modulus, shares_ptr, n, dim, row_stride, out_ptr, stream=None):
+        _check(self.lib.sda_combine_dev(self.h, modulus, shares_ptr, n, dim, row_stride, out_ptr, stream))
+
+    def combine_finalize_dev(self, modulus, sums_ptr, dim, out_ptr, stream=None):
+        _check(self.lib.sda_combine_finalize_dev(self.h, modulus, sums_ptr, dim, out_ptr, stream))
+
+    def packed_generate_dev(self, scheme, secrets_ptr, dimension, n_vectors, draws_ptr, out_ptr, stream=None):
+        s = scheme.c()
+        _check(self.lib.sda_packed_generate_dev(self.h, C.byref(s), secrets_ptr, dimension, n_vectors, draws_ptr,
+                                                out_ptr, stream))
+
+    def packed_reconstruct_dev(self, scheme, dimension, indices, n_vectors, shares_ptr, out_ptr,
+                               mode=REVEAL_EXACT, stream=None):
+        s = scheme.c()
+        idx = _arr(indices, np.uint64)
+        _check(self.lib.sda_packed_reconstruct_dev(self.h, C.byref(s), dimension, _ptr(idx, _u64p), idx.size,
+                                                   n_vectors, shares_ptr, out_ptr, mode, stream))
+
+    def additive_generate_dev(self, modulus, share_count, secrets_ptr, dimension, draws_ptr, out_ptr, stream=None):
+        _check(self.lib.sda_additive_generate_dev(self.h, modulus, share_count, secrets_ptr, dimension, draws_ptr,
+                                                  out_ptr, stream))
+
+    def chacha_mask_combine_dev(self, modulus, dimension, seeds_ptr, w, n_seeds, out_ptr, stream=None):
+        _check(self.lib.sda_chacha_mask_combine_dev(self.h, modulus, dimension, seeds_ptr, w, n_seeds, out_ptr,
+                                                    stream))
+
+    def synth_fill_dev(self, dst_ptr, rows, cols, seed, lo, hi, stream=None):
+        _check(self.lib.sda_synth_fill_dev(self.h, dst_ptr, rows, cols, seed, lo, hi, stream))

@@ -1,0 +1,130 @@
+"""GPU: device-resident entry points (the ones bench.py times) at larger sizes.
+
+Full-size results are checked through properties that do not need the oracle to finish the
+whole job: column independence (the oracle recomputes a random sample of columns / batches
+exactly), encode -> decode round trips, and torch int64 column sums for non-negative inputs.
+"""
+import numpy as np
+import pytest
+
+from sda_amd import schemes as S
+from sda_amd import engine as E
+from sda_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+def test_synth_fill_matches_numpy(engine):
+    rows, cols, seed, lo, hi = 37, 1001, 0x5DA + 2, -2147482800, 2147482801
+    t = torch.empty((rows, cols), dtype=torch.int64, device="cuda")
+    engine.synth_fill_dev(t.data_ptr(), rows, cols, seed, lo, hi, _stream())
+    torch.cuda.synchronize()
+    assert (t.cpu().numpy() == synth.fill(rows, cols, seed, lo, hi)).all()
+
+
+@pytest.mark.parametrize("dim,stride", [(1_000_000, 1_000_000), (1_000_003, 1_000_003), (500_000, 500_016)])
+def test_combine_dev_large(engine, oracle, dim, stride):
+    m, N = 2147482801, 1024
+    x = torch.empty((N, stride), dtype=torch.int64, device="cuda")
+    # signed inputs in (-m, m): the order-dependent case
+    engine.synth_fill_dev(x.data_ptr(), N, stride, 0x5DA + 9, -(m - 1), m, _stream())
+    out = torch.empty(dim, dtype=torch.int64, device="cuda")
+    engine.combine_dev(m, x.data_ptr(), N, dim, stride, out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    cols = np.random.default_rng(dim).choice(dim, 512, replace=False)
+    xs = x[:, torch.from_numpy(cols).cuda()].cpu().numpy()
+    assert got[cols].tolist() == oracle.combine(m, xs).tolist()
+    # property: residue equals the column sum mod m
+    col_sum = x[:, :dim].sum(dim=0)           # |sum| < N * m < 2^63
+    assert (torch.remainder(col_sum, m).cpu().numpy() == np.mod(got, m)).all()
+
+
+def test_combine_dev_canonical_and_finalize(engine):
+    m, N, D = 2147482801, 512, 1_000_000
+    x = torch.empty((N, D), dtype=torch.int64, device="cuda")
+    engine.synth_fill_dev(x.data_ptr(), N, D, 0x5DA + 1, 0, m, _stream())
+    out = torch.empty(D, dtype=torch.int64, device="cuda")
+    engine.combine_dev(m, x.data_ptr(), N, D, D, out.data_ptr(), _stream())
+    exp = torch.remainder(x.sum(dim=0), m)
+    torch.cuda.synchronize()
+    assert torch.equal(out, exp)
+    # two "ranks": halves combined separately, summed as int64, finalized on device
+    a = torch.empty(D, dtype=torch.int64, device="cuda")
+    b = torch.empty(D, dtype=torch.int64, device="cuda")
+    engine.combine_dev(m, x.data_ptr(), N // 2, D, D, a.data_ptr(), _stream())
+    engine.combine_dev(m, x[N // 2:].data_ptr(), N - N // 2, D, D, b.data_ptr(), _stream())
+    s = a + b
+    fin = torch.empty(D, dtype=torch.int64, device="cuda")
+    engine.combine_finalize_dev(m, s.data_ptr(), D, fin.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    assert torch.equal(fin, exp)
+
+
+@pytest.mark.parametrize("mode", [E.REVEAL_EXACT, E.REVEAL_CANONICAL])
+def test_packed_dev_roundtrip_config(engine, oracle, mode):
+    """configs[2]: k=8, n=26, t=7 at 1M-dim, several participant vectors per launch."""
+    sch = S.CONFIG_PACKED
+    p, k, t, n = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count
+    V, D = 3, 1_000_000
+    B = D // k
+    sec = torch.empty((V, D), dtype=torch.int64, device="cuda")
+    engine.synth_fill_dev(sec.data_ptr(), V, D, 0x5DA + 2, 0, p, _stream())
+    draws = torch.empty((V, B, t), dtype=torch.int64, device="cuda")
+    engine.synth_fill_dev(draws.data_ptr(), V * B, t, 0x5DA + 22, 0, p - 1, _stream())
+    shares = torch.empty((V, n, B), dtype=torch.int64, device="cuda")
+    engine.packed_generate_dev(sch, sec.data_ptr(), D, V, draws.data_ptr(), shares.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    # batches are independent: check a sample against the oracle (tss op order, signed)
+    pp = oracle.packed_params(k, n, t, p, sch.omega_secrets, sch.omega_shares)
+    sec_h, dr_h, sh_h = sec.cpu().numpy(), draws.cpu().numpy(), shares.cpu().numpy()
+    for v, b in zip(np.random.default_rng(1).integers(0, V, 64), np.random.default_rng(2).integers(0, B, 64)):
+        exp = oracle.packed_share(pp, sec_h[v, b * k:(b + 1) * k], dr_h[v, b])
+        assert sh_h[v, :, b].tolist() == exp.tolist()
+    # reveal from a t+k subset (reversed) and from all clerks: round trip to the secrets
+    for idx in (list(range(n - 1, n - 1 - (t + k), -1)), list(range(n))):
+        sub = shares[:, idx, :].contiguous()
+        out = torch.empty((V, D), dtype=torch.int64, device="cuda")
+        engine.packed_reconstruct_dev(sch, D, idx, V, sub.data_ptr(), out.data_ptr(), mode, _stream())
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert (np.mod(got, p) == sec_h).all()
+        if mode == E.REVEAL_CANONICAL:
+            assert got.min() >= 0
+        else:
+            # exact representatives on a batch sample
+            for v, b in zip(range(V), (5, B // 2, B - 1)):
+                rc, exp = oracle.packed_reconstruct(pp, k, idx, sh_h[v][idx][:, b:b + 1])
+                assert got[v, b * k:(b + 1) * k].tolist() == exp.tolist()
+
+
+def test_chacha_combine_dev(engine, oracle):
+    m, D, N = 2147482801, 100_003, 48
+    seeds = np.random.default_rng(3).integers(0, 2**32, size=(N, 4), dtype=np.uint64).astype(np.uint32)
+    out = torch.empty(D, dtype=torch.int64, device="cuda")
+    sd = _dev(seeds.view(np.int32)).view(torch.int32)
+    engine.chacha_mask_combine_dev(m, D, sd.data_ptr(), 4, N, out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tolist() == oracle.chacha_mask_combine(m, D, seeds.astype(np.int64)).tolist()
+
+
+def test_additive_generate_dev(engine, oracle):
+    m, n, D = 433, 3, 200_001
+    rng = np.random.default_rng(4)
+    sec = rng.integers(-(2**40), 2**40, size=D, dtype=np.int64)
+    draws = rng.integers(0, m, size=D * (n - 1), dtype=np.int64)
+    out = torch.empty((n, D), dtype=torch.int64, device="cuda")
+    dsec, ddr = _dev(sec), _dev(draws)          # keep the device buffers alive across the launch
+    engine.additive_generate_dev(m, n, dsec.data_ptr(), D, ddr.data_ptr(), out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy() == oracle.additive_generate(m, n, sec, draws)).all()

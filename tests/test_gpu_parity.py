@@ -1,0 +1,306 @@
+"""GPU parity: the MI355X engine (through the C ABI) against the CPU oracle and golden fixtures.
+
+Bar: bit-exact (integer work).  Sizes are ones the oracle finishes in seconds; the full-size
+configurations are covered by size-independent properties in test_gpu_device.py.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from sda_amd import SdaError, schemes as S
+from sda_amd import engine as E
+from tests.oracle_backend import OracleBackend
+from tests.pipeline import (FULL_LOOP_EXPECTED, FULL_LOOP_INPUTS, README_EXPECTED, README_INPUTS, Draws,
+                            full_loop_variants, run_aggregation)
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+I64_MIN, I64_MAX = -(2**63), 2**63 - 1
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def _pp(O, sch):
+    return O.packed_params(sch.secret_count, sch.share_count, sch.privacy_threshold(), sch.prime_modulus,
+                           sch.omega_secrets, sch.omega_shares)
+
+
+# ------------------------------------------------------------------ end-to-end KATs
+@pytest.mark.parametrize("variant", list(full_loop_variants()))
+def test_full_loop_kat_trace(engine, variant):
+    """Every stage of integration-tests/tests/full_loop.rs, bit-exact against the golden trace."""
+    v = load("full_loop_kat.json")[variant]
+    masking, sharing = full_loop_variants()[variant]
+    tr = run_aggregation(engine, masking, sharing, 433, 4, v["inputs"], Draws(v["draw_seed"]))
+    t = v["trace"]
+    assert [m.tolist() for m in tr.masks] == t["masks"]
+    assert [m.tolist() for m in tr.masked] == t["masked"]
+    assert [s.tolist() for s in tr.shares] == t["shares"]
+    assert [c.tolist() for c in tr.clerk_results] == t["clerk_results"]
+    assert (None if tr.combined_mask is None else tr.combined_mask.tolist()) == t["combined_mask"]
+    assert tr.masked_output.tolist() == t["masked_output"]
+    assert tr.output.tolist() == t["output"]
+    assert tr.positive.tolist() == FULL_LOOP_EXPECTED
+
+
+@pytest.mark.parametrize("variant", list(full_loop_variants()))
+def test_full_loop_kat_many_draws(engine, oracle, variant):
+    masking, sharing = full_loop_variants()[variant]
+    for seed in range(4):
+        a = run_aggregation(engine, masking, sharing, 433, 4, FULL_LOOP_INPUTS, Draws(seed))
+        b = run_aggregation(OracleBackend(), masking, sharing, 433, 4, FULL_LOOP_INPUTS, Draws(seed))
+        assert a.masked_output.tolist() == b.masked_output.tolist()
+        assert a.positive.tolist() == FULL_LOOP_EXPECTED
+
+
+def test_full_loop_packed_subsets(engine, oracle):
+    masking, sharing = full_loop_variants()["with_packedshamir"]
+    for order in ([0, 2, 3, 4, 5, 6, 7], [7, 6, 5, 4, 3, 1, 0], [1, 2, 3, 4, 5, 6, 7]):
+        a = run_aggregation(engine, masking, sharing, 433, 4, FULL_LOOP_INPUTS, Draws(7), clerk_order=order)
+        b = run_aggregation(OracleBackend(), masking, sharing, 433, 4, FULL_LOOP_INPUTS, Draws(7), clerk_order=order)
+        assert a.masked_output.tolist() == b.masked_output.tolist()
+        assert a.positive.tolist() == FULL_LOOP_EXPECTED
+
+
+def test_readme_walkthrough(engine):
+    v = load("readme_walkthrough.json")
+    tr = run_aggregation(engine, S.NoMasking(), S.Additive(3, 433), 433, 10, README_INPUTS, Draws(v["draw_seed"]))
+    assert [c.tolist() for c in tr.clerk_results] == v["trace"]["clerk_results"]
+    assert tr.positive.tolist() == README_EXPECTED
+
+
+# ------------------------------------------------------------------ combine (north-star kernel 1)
+def test_combine_golden_cases(engine):
+    for c in load("combine_cases.json"):
+        got = engine.share_combine(S.Additive(3, c["m"]), c["rows"])
+        assert got.tolist() == c["expected"], c
+
+
+@pytest.mark.parametrize("m", [433, 2147482801, 1, 2, (1 << 40) + 7, (1 << 62) + 3, I64_MAX])
+@pytest.mark.parametrize("N,D", [(1, 1), (3, 10), (17, 1001), (64, 4096), (300, 2049), (2, 100003)])
+def test_combine_random(engine, oracle, m, N, D):
+    rng = np.random.default_rng(N * 7919 + D + m % 1000)
+    for kind in ("canonical", "signed", "wide"):
+        if kind == "canonical":
+            x = rng.integers(0, m, size=(N, D), dtype=np.int64, endpoint=False)
+        elif kind == "signed":
+            x = rng.integers(-(m - 1), m, size=(N, D), dtype=np.int64) if m > 1 else np.zeros((N, D), np.int64)
+        else:
+            x = rng.integers(I64_MIN, I64_MAX, size=(N, D), dtype=np.int64, endpoint=True)
+        got = engine.share_combine(S.Additive(3, m), list(x))
+        assert got.tolist() == oracle.combine(m, x).tolist(), kind
+
+
+def test_combine_negative_modulus_and_errors(engine, oracle):
+    x = np.array([[5, -7, 12], [9, 3, -20]], np.int64)
+    assert engine.share_combine(S.Additive(3, -10), list(x)).tolist() == oracle.combine(-10, x).tolist()
+    assert engine.share_combine(S.Additive(3, 433), []).tolist() == []
+    with pytest.raises(SdaError) as ei:
+        engine.share_combine(S.Additive(3, 433), [[1, 2], [3]])
+    assert ei.value.status == E.ERR_WRONG_DIMENSION and str(ei.value).startswith("Wrong dimension")
+    with pytest.raises(SdaError) as ei:
+        engine.share_combine(S.Additive(3, 0), [[1, 2]])
+    assert ei.value.status == E.ERR_PRECONDITION
+
+
+def test_additive_reconstruct_is_combine(engine, oracle):
+    rows = [np.array([1, -2, 400]), np.array([432, 5, 100]), np.array([-431, 0, -1])]
+    got = engine.secret_reconstruct(S.Additive(3, 433), 3, [(2, rows[0]), (0, rows[1]), (1, rows[2])])
+    assert got.tolist() == oracle.combine(433, np.stack(rows)).tolist()
+    with pytest.raises(SdaError) as ei:
+        engine.secret_reconstruct(S.Additive(3, 433), 3, [(0, [1, 2]), (1, [1])])
+    assert ei.value.status == E.ERR_MISMATCHING_DIMENSION
+
+
+# ------------------------------------------------------------------ additive generate
+def test_additive_fixture(engine):
+    a = load("additive_cases.json")
+    got = engine.share_generate(S.Additive(a["n"], a["m"]), a["secrets"], a["draws"])
+    assert got.tolist() == a["expected"]
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 26])
+@pytest.mark.parametrize("m", [433, 2147482801, (1 << 62) + 3])
+def test_additive_generate_random(engine, oracle, n, m):
+    rng = np.random.default_rng(n * 31 + m % 97)
+    D = 5000
+    secrets = rng.integers(I64_MIN, I64_MAX, size=D, dtype=np.int64, endpoint=True)
+    secrets[: D // 2] = rng.integers(-(m - 1), m, size=D // 2, dtype=np.int64)
+    draws = rng.integers(0, m, size=D * (n - 1), dtype=np.int64)
+    got = engine.share_generate(S.Additive(n, m), secrets, draws)
+    assert got.tolist() == oracle.additive_generate(m, n, secrets, draws).tolist()
+
+
+# ------------------------------------------------------------------ packed Shamir (north-star kernel 2)
+def _roots(p, L, N3):
+    """order-L and order-N3 roots of unity mod p (smallest generator)."""
+    fac, x, d = set(), p - 1, 2
+    while d * d <= x:
+        while x % d == 0:
+            fac.add(d)
+            x //= d
+        d += 1
+    if x > 1:
+        fac.add(x)
+    g = next(g for g in range(2, p) if all(pow(g, (p - 1) // q, p) != 1 for q in fac))
+    return pow(g, (p - 1) // L, p), pow(g, (p - 1) // N3, p)
+
+
+def _prime_for(L, N3, below=2**31):
+    step = L * N3 // np.gcd(L, N3)
+    c = (below - 1) // step
+    while True:
+        p = c * step + 1
+        if p < below and all(p % q for q in range(2, int(p**0.5) + 1)):
+            return p
+        c -= 1
+
+
+def packed_schemes():
+    out = [S.FULL_LOOP_PACKED, S.CONFIG_PACKED]
+    for k, t, n in [(1, 0, 2), (3, 4, 26), (7, 8, 26), (1, 1, 8), (15, 16, 80), (8, 7, 80), (31, 32, 80)]:
+        L, N3 = k + t + 1, n + 1
+        p = _prime_for(L, N3) if (L, N3) != (8, 27) else 433
+        ws, wn = _roots(p, L, N3)
+        out.append(S.PackedShamir(k, n, t, p, ws, wn))
+    return out
+
+
+def test_packed_fixture(engine):
+    for c in load("packed_cases.json"):
+        p = c["scheme"]["PackedShamir"]
+        sch = S.PackedShamir(p["secret_count"], p["share_count"], p["privacy_threshold"], p["prime_modulus"],
+                             p["omega_secrets"], p["omega_shares"])
+        shares = engine.share_generate(sch, c["secrets"], c["draws"])
+        assert shares.tolist() == c["shares"]
+        for r in c["reveals"]:
+            got = engine.secret_reconstruct(sch, len(c["secrets"]), [(i, shares[i]) for i in r["indices"]])
+            assert got.tolist() == r["expected"]
+
+
+@pytest.mark.parametrize("sch", packed_schemes(), ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")
+def test_packed_generate_random(engine, oracle, sch):
+    p = sch.prime_modulus
+    rng = np.random.default_rng(p % 1000 + sch.share_count)
+    D = 37 * sch.secret_count + 1 if sch.secret_count > 1 else 300
+    B = (D + sch.secret_count - 1) // sch.secret_count
+    secrets = rng.integers(-(p - 1), p, size=D, dtype=np.int64)
+    draws = rng.integers(0, p - 1, size=B * sch.privacy_threshold(), dtype=np.int64)
+    got = engine.share_generate(sch, secrets, draws)
+    exp = oracle.packed_generate(_pp(oracle, sch), secrets, draws)
+    assert got.tolist() == exp.tolist()
+    # raw i64 secrets outside (-p, p): generic exact path (wrapping i64, tss order)
+    wide = secrets.copy()
+    wide[::5] = rng.integers(-(2**40), 2**40, size=wide[::5].size, dtype=np.int64)
+    got = engine.share_generate(sch, wide, draws)
+    assert got.tolist() == oracle.packed_generate(_pp(oracle, sch), wide, draws).tolist()
+
+
+@pytest.mark.parametrize("sch", packed_schemes(), ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")
+def test_packed_reconstruct_random(engine, oracle, sch):
+    p, n = sch.prime_modulus, sch.share_count
+    if n > 63:
+        n_max = 63
+    else:
+        n_max = n
+    rng = np.random.default_rng(p % 777 + n)
+    D = 23 * sch.secret_count + 1
+    B = (D + sch.secret_count - 1) // sch.secret_count
+    secrets = rng.integers(0, p, size=D, dtype=np.int64)
+    draws = rng.integers(0, p - 1, size=B * sch.privacy_threshold(), dtype=np.int64)
+    shares = oracle.packed_generate(_pp(oracle, sch), secrets, draws)
+    need = sch.reconstruction_threshold()
+    for trial in range(4):
+        size = int(rng.integers(need, n_max + 1))
+        idx = rng.permutation(n)[:size].tolist()
+        got = engine.secret_reconstruct(sch, D, [(i, shares[i]) for i in idx])
+        rc, exp = oracle.packed_reconstruct(_pp(oracle, sch), D, idx, shares[idx])
+        assert rc == 0
+        assert got.tolist() == exp.tolist()
+        assert (got % p == secrets % p).all()
+    # shares outside (-p, p) (e.g. combined shares fed in raw): generic exact path
+    idx = list(range(need))
+    raw = shares[idx].copy()
+    raw[0, ::3] += 5 * p
+    got = engine.secret_reconstruct(sch, D, [(i, raw[j]) for j, i in enumerate(idx)])
+    rc, exp = oracle.packed_reconstruct(_pp(oracle, sch), D, idx, raw)
+    assert got.tolist() == exp.tolist()
+
+
+def test_packed_errors(engine):
+    sch = S.FULL_LOOP_PACKED
+    shares = engine.share_generate(sch, [1, 2, 3], [1, 2, 3, 4])
+    with pytest.raises(SdaError) as ei:
+        engine.secret_reconstruct(sch, 3, [(i, shares[i]) for i in range(6)])
+    assert ei.value.status == E.ERR_NOT_ENOUGH_SHARES
+    assert engine.secret_reconstruct(sch, 0, [(0, [])]).tolist() == []     # no batch => no check
+    with pytest.raises(SdaError) as ei:
+        engine.share_generate(S.PackedShamir(3, 8, 5, 433, 354, 150), [1, 2, 3], [0] * 5)
+    assert ei.value.status == E.ERR_UNSUPPORTED                             # L = 9 not a power of 2
+
+
+# ------------------------------------------------------------------ masking (north-star kernel 3)
+@pytest.mark.parametrize("m", [433, 2147482801, (1 << 40) + 7, (1 << 62) + 1])
+@pytest.mark.parametrize("words", [0, 1, 4, 8, 10])
+def test_chacha_mask_and_combine(engine, oracle, m, words):
+    rng = np.random.default_rng(m % 991 + words)
+    D = 1000 if m > (1 << 61) else 3001
+    sch = S.ChaChaMasking(m, D, 32 * words)
+    secrets = rng.integers(0, m, size=D, dtype=np.int64)
+    seeds = [rng.integers(0, 2**32, size=words, dtype=np.uint64).astype(np.uint32) for _ in range(5)]
+    for sd in seeds[:2]:
+        mask, masked = engine.secret_mask(sch, secrets, seed=sd)
+        assert mask.tolist() == sd.astype(np.int64).tolist()
+        assert masked.tolist() == oracle.chacha_mask(m, sd, secrets).tolist()
+    rows = [sd.astype(np.int64) for sd in seeds]
+    got = engine.mask_combine(sch, rows)
+    exp = oracle.chacha_mask_combine(m, D, np.stack(rows) if words else np.zeros((5, 0), np.int64))
+    assert got.tolist() == exp.tolist()
+
+
+def test_chacha_many_seeds(engine, oracle):
+    m, D, N = 2147482801, 777, 300
+    rng = np.random.default_rng(5)
+    rows = [rng.integers(0, 2**32, size=4, dtype=np.uint64).astype(np.int64) for _ in range(N)]
+    got = engine.mask_combine(S.ChaChaMasking(m, D, 128), rows)
+    assert got.tolist() == oracle.chacha_mask_combine(m, D, np.stack(rows)).tolist()
+
+
+def test_chacha_ragged_seed_lengths(engine, oracle):
+    m, D = 433, 100
+    rows = [np.array([1, 2, 3, 4]), np.array([5]), np.array([], np.int64), np.array([7, 8])]
+    got = engine.mask_combine(S.ChaChaMasking(m, D, 128), rows)
+    padded = np.zeros((4, 4), np.int64)
+    for i, r in enumerate(rows):
+        padded[i, : len(r)] = r
+    assert got.tolist() == oracle.chacha_mask_combine(m, D, padded).tolist()
+
+
+def test_chacha_dimension_assert(engine):
+    with pytest.raises(SdaError) as ei:
+        engine.secret_mask(S.ChaChaMasking(433, 5, 128), [1, 2, 3], seed=[1, 2, 3, 4])
+    assert ei.value.status == E.ERR_PRECONDITION
+
+
+@pytest.mark.parametrize("m", [433, 2147482801, (1 << 62) + 3])
+def test_full_mask_unmask_positive(engine, oracle, m):
+    rng = np.random.default_rng(m % 313)
+    D = 4097
+    secrets = rng.integers(I64_MIN // 2, I64_MAX // 2, size=D, dtype=np.int64)
+    masks = rng.integers(0, m, size=D, dtype=np.int64)
+    mk, masked = engine.secret_mask(S.FullMasking(m), secrets, full_masks=masks)
+    assert mk.tolist() == masks.tolist()
+    assert masked.tolist() == oracle.full_mask(m, masks, secrets).tolist()
+    rows = [rng.integers(0, m, size=D, dtype=np.int64) for _ in range(7)]
+    assert engine.mask_combine(S.FullMasking(m), rows).tolist() == oracle.combine(m, np.stack(rows)).tolist()
+    un = engine.secret_unmask(S.FullMasking(m), (masks, masked))
+    assert un.tolist() == oracle.unmask(m, masks, masked).tolist()
+    assert engine.positive(m, un).tolist() == oracle.positive(m, un).tolist()
+    assert engine.secret_unmask(S.NoMasking(), ([], secrets)).tolist() == secrets.tolist()
+    with pytest.raises(SdaError):
+        engine.secret_unmask(S.FullMasking(m), (masks[:-1], masked))
