@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __r
 }
 
 // Fix one stream: for elements i >= i0, replace draw(pair i) by draw(pair a_i), where a_i is the
-// i-th non-rejected pair: a_i = i + #{r in rej : r <= a_i}.  acc stays unsigned: += new + m - old.
+// i-th non-rejected pair: a_i = i + #{r in rej : r <= a_i}.  acc[i] <- (acc[i] + new - old) mod m.
 __global__ __launch_bounds__(256) void chacha_fix_kernel(Key8 key, uint64_t i0, uint64_t D,
                                                          const uint64_t* __restrict__ rej, uint32_t n_rej,
                                                          unsigned long long* __restrict__ acc, Mod64 M) {
@@ -120,11 +120,15 @@ __global__ __launch_bounds__(256) void chacha_fix_kernel(Key8 key, uint64_t i0, 
     const uint64_t vo = ((uint64_t)o[2 * (i % 8)] << 32) | o[2 * (i % 8) + 1];
     chacha_block(key.k, ai / 8, o);
     const uint64_t vn = ((uint64_t)o[2 * (ai % 8)] << 32) | o[2 * (ai % 8) + 1];
-    acc[i] += (unsigned long long)(umod64(vn, M) + (M.m - umod64(vo, M)));
+    // acc[i] is canonical here (acc_mod_kernel ran in place first): stay in [0, m)
+    uint64_t a = acc[i] + umod64(vn, M);          // < 2m <= 2^64 - 2
+    a = a >= M.m ? a - M.m : a;
+    const uint64_t od = umod64(vo, M);
+    acc[i] = a >= od ? a - od : a + (M.m - od);
 }
 
-__global__ __launch_bounds__(256) void acc_mod_kernel(const unsigned long long* __restrict__ acc, uint64_t D,
-                                                      int64_t* __restrict__ out, Mod64 M) {
+__global__ __launch_bounds__(256) void acc_mod_kernel(const unsigned long long* acc, uint64_t D,
+                                                      int64_t* out, Mod64 M) {   // may run in place
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < D) out[i] = (int64_t)umod64(acc[i], M);
 }
@@ -183,6 +187,8 @@ static hipError_t chacha_combine_impl(int64_t modulus, uint64_t D, const uint32_
     uint64_t chunks = (2048 + gx - 1) / gx;
     if (chunks > n_seeds) chunks = n_seeds ? n_seeds : 1;
     if (chunks > 65535) chunks = 65535;
+    // headroom: the u64 accumulators receive one canonical partial (< m) per chunk
+    if (M.m > 1 && chunks > UINT64_MAX / (M.m - 1)) chunks = UINT64_MAX / (M.m - 1);
     const uint64_t per = n_seeds ? (n_seeds + chunks - 1) / chunks : 0;
     RejectLog log{count, seed_of, pair_of, kRejectCap};
     if (n_seeds) {
@@ -195,6 +201,10 @@ static hipError_t chacha_combine_impl(int64_t modulus, uint64_t D, const uint32_
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
         if (n_rej > kRejectCap) return hipErrorOutOfMemory;   // engine falls back (see engine.cpp)
         if (n_rej) {
+            // canonicalise in place so the fix-ups can work modulo m without overflow
+            hipLaunchKernelGGL(acc_mod_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, acc, D,
+                               reinterpret_cast<int64_t*>(acc), M);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
             std::vector<uint32_t> so(n_rej);
             std::vector<uint64_t> po(n_rej);
             if ((e = hipMemcpy(so.data(), seed_of, n_rej * 4, hipMemcpyDeviceToHost)) != hipSuccess) return e;

@@ -24,6 +24,8 @@ struct sda_engine {
     size_t work_bytes = 0;
     void* stage = nullptr;        // staging for host-path inputs/outputs
     size_t stage_bytes = 0;
+    sda::DeviceTable gen_tab;     // packed-Shamir twiddles (per scheme)
+    sda::DeviceTable rev_tab;     // packed-Shamir Newton/Lagrange tables (per scheme + clerk set)
 };
 
 namespace {
@@ -192,6 +194,8 @@ void sda_engine_destroy(sda_engine* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->work) (void)hipFree(h->work);
     if (h->stage) (void)hipFree(h->stage);
+    sda::free_table(h->gen_tab);
+    sda::free_table(h->rev_tab);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -262,7 +266,8 @@ sda_status sda_share_generate(sda_engine* h, const sda_sharing_scheme* s, const 
     if (n_draws) HIP_TRY(hipMemcpyAsync(ddr, draws, n_draws * 8, hipMemcpyHostToDevice, h->stream));
     sda::PackedGenArgs ga{dsec, D, 1, ddr, dout};
     HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)k, (uint32_t)t, (uint32_t)n, (uint32_t)s->modulus,
-                                        (uint32_t)s->omega_secrets, (uint32_t)s->omega_shares, h->stream));
+                                        (uint32_t)s->omega_secrets, (uint32_t)s->omega_shares, h->gen_tab,
+                                        h->stream));
     HIP_TRY(hipMemcpyAsync(out, dout, n * B * 8, hipMemcpyDeviceToHost, h->stream));
     return finish(h);
 }
@@ -336,17 +341,15 @@ sda_status sda_secret_reconstruct(sda_engine* h, const sda_sharing_scheme* s, ui
                     (unsigned long long)n_rows, (unsigned long long)(s->privacy_threshold + k));
     if (n_rows > 63) return fail(SDA_ERR_UNSUPPORTED, "more than 63 clerk shares per batch");
     DevArena a;
-    const size_t tab = sda::packed_reveal_scratch_bytes((uint32_t)n_rows, (uint32_t)k);
-    if (sda_status st = stage(h, rup(n_rows * B * 8) + rup(dimension * 8) + rup(tab), &a)) return st;
+    if (sda_status st = stage(h, rup(n_rows * B * 8) + rup(dimension * 8), &a)) return st;
     int64_t* din = a.take<int64_t>(n_rows * B);
     int64_t* dout = a.take<int64_t>(dimension);
-    int64_t* dtab = a.take<int64_t>(tab / 8 + 1);
     for (uint64_t i = 0; i < n_rows; ++i)
         HIP_TRY(hipMemcpyAsync(din + i * B, rows[i], B * 8, hipMemcpyHostToDevice, h->stream));
     sda::PackedRevealArgs ra{din, dimension, 1, dout};
-    HIP_TRY(sda::launch_packed_reveal(ra, indices, (uint32_t)n_rows, (uint32_t)k, (uint32_t)s->privacy_threshold,
-                                      (uint32_t)s->share_count, (uint32_t)s->modulus, (uint32_t)s->omega_secrets,
-                                      (uint32_t)s->omega_shares, SDA_REVEAL_EXACT, dtab, h->stream));
+    HIP_TRY(sda::launch_packed_reveal(ra, indices, (uint32_t)n_rows, (uint32_t)k, (uint32_t)s->modulus,
+                                      (uint32_t)s->omega_secrets, (uint32_t)s->omega_shares, SDA_REVEAL_EXACT,
+                                      h->rev_tab, h->stream));
     HIP_TRY(hipMemcpyAsync(out, dout, dimension * 8, hipMemcpyDeviceToHost, h->stream));
     *out_len = dimension;
     return finish(h);
@@ -529,7 +532,7 @@ sda_status sda_packed_generate_dev(sda_engine* h, const sda_sharing_scheme* s, c
     sda::PackedGenArgs ga{secrets, dimension, n_vectors, draws, out};
     HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)s->secret_count, (uint32_t)s->privacy_threshold,
                                         (uint32_t)s->share_count, (uint32_t)s->modulus, (uint32_t)s->omega_secrets,
-                                        (uint32_t)s->omega_shares, pick(h, stream)));
+                                        (uint32_t)s->omega_shares, h->gen_tab, pick(h, stream)));
     return ok();
 }
 
@@ -544,13 +547,10 @@ sda_status sda_packed_reconstruct_dev(sda_engine* h, const sda_sharing_scheme* s
     if (n_idx > 63) return fail(SDA_ERR_UNSUPPORTED, "more than 63 clerk shares per batch");
     if (n_vectors > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 vectors per launch");
     HIP_TRY(hipSetDevice(h->device));
-    const size_t tab = sda::packed_reveal_scratch_bytes((uint32_t)n_idx, (uint32_t)s->secret_count);
-    if (sda_status st = ensure(&h->work, &h->work_bytes, tab)) return st;
     sda::PackedRevealArgs ra{shares, dimension, n_vectors, out};
     hipError_t e = sda::launch_packed_reveal(ra, indices, (uint32_t)n_idx, (uint32_t)s->secret_count,
-                                             (uint32_t)s->privacy_threshold, (uint32_t)s->share_count,
                                              (uint32_t)s->modulus, (uint32_t)s->omega_secrets,
-                                             (uint32_t)s->omega_shares, mode, (int64_t*)h->work, pick(h, stream));
+                                             (uint32_t)s->omega_shares, mode, h->rev_tab, pick(h, stream));
     if (e == hipErrorInvalidValue && mode == SDA_REVEAL_CANONICAL)
         return fail(SDA_ERR_UNSUPPORTED, "canonical reveal needs distinct clerk indices");
     HIP_TRY(e);

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "modarith.h"
 
 namespace sda {
@@ -27,23 +29,30 @@ hipError_t launch_positive(const int64_t* v, uint64_t D, int64_t* out, int64_t m
 hipError_t launch_synth_fill(int64_t* dst, uint64_t rows, uint64_t cols, uint64_t seed,
                              int64_t lo, int64_t hi, hipStream_t s);
 
-// ---- packed_shamir.hip ----
-struct PackedPlan;   // defined in packed_shamir.hip (twiddles, Montgomery constants)
+// ---- packed_gen.hip / packed_reveal.hip ----
+// Engine-owned device copy of a precomputed, data-independent table (twiddles, Newton inverses,
+// Lagrange weights).  Rebuilt and uploaded only when its key (the parameters it depends on) changes.
+struct DeviceTable {
+    std::vector<uint8_t> key;
+    void* dev = nullptr;
+    size_t cap = 0;
+};
+hipError_t ensure_table(DeviceTable& t, const std::vector<uint8_t>& key, const void* host, size_t bytes);
+void free_table(DeviceTable& t);
+
 struct PackedGenArgs {
     const int64_t* secrets; uint64_t dimension; uint64_t n_vectors;
     const int64_t* draws; int64_t* out;
 };
-hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t, uint32_t n,
-                                  uint32_t p, uint32_t omega_secrets, uint32_t omega_shares,
-                                  hipStream_t s);
+hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t, uint32_t n, uint32_t p,
+                                  uint32_t omega_secrets, uint32_t omega_shares, DeviceTable& tab, hipStream_t s);
 struct PackedRevealArgs {
     const int64_t* shares; uint64_t dimension; uint64_t n_vectors; int64_t* out;
 };
-hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indices, uint32_t n_idx,
-                                uint32_t k, uint32_t t, uint32_t n, uint32_t p,
-                                uint32_t omega_secrets, uint32_t omega_shares, int mode,
-                                int64_t* scratch_dev, hipStream_t s);
-size_t packed_reveal_scratch_bytes(uint32_t n_idx, uint32_t k);
+// returns hipErrorInvalidValue for CANONICAL mode with duplicate clerk points
+hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indices, uint32_t n_idx, uint32_t k,
+                                uint32_t p, uint32_t omega_secrets, uint32_t omega_shares, int mode,
+                                DeviceTable& tab, hipStream_t s);
 
 // ---- chacha.hip ----
 // Combine of n_seeds ChaCha mask streams (chacha.rs:57-76).  `work` must hold

@@ -69,7 +69,8 @@ template <int L, int N3>
 __global__ __launch_bounds__(256) void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D,
                                                          const int64_t* __restrict__ draws,
                                                          int64_t* __restrict__ out, uint32_t k, uint32_t t,
-                                                         uint64_t B, const GenTables T) {
+                                                         uint64_t B, const GenTables* __restrict__ Tp) {
+    const GenTables& T = *Tp;          // global memory: uniform => scalar loads, no per-lane copy
     constexpr int LB = ilog(L, 2);
     constexpr int ND = ilog(N3, 3);
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(256) void packed_gen_kernel(const int64_t* __restri
 }  // namespace
 
 template <int L, int N3>
-static hipError_t gen_launch(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables& T,
+static hipError_t gen_launch(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
                              hipStream_t s) {
     dim3 grid((unsigned)((B + 255) / 256), (unsigned)a.n_vectors);
     hipLaunchKernelGGL((packed_gen_kernel<L, N3>), grid, dim3(256), 0, s, a.secrets, a.dimension, a.draws, a.out,
@@ -155,7 +156,7 @@ static hipError_t gen_launch(const PackedGenArgs& a, uint32_t k, uint32_t t, uin
 
 template <int N3>
 static hipError_t gen_dispatch_L(uint32_t L, const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B,
-                                 const GenTables& T, hipStream_t s) {
+                                 const GenTables* T, hipStream_t s) {
     switch (L) {
         case 2: return gen_launch<2, N3>(a, k, t, B, T, s);
         case 4: if constexpr (N3 >= 4) return gen_launch<4, N3>(a, k, t, B, T, s); break;
@@ -168,11 +169,18 @@ static hipError_t gen_dispatch_L(uint32_t L, const PackedGenArgs& a, uint32_t k,
 }
 
 hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t, uint32_t n, uint32_t p,
-                                  uint32_t omega_secrets, uint32_t omega_shares, hipStream_t s) {
+                                  uint32_t omega_secrets, uint32_t omega_shares, DeviceTable& tab, hipStream_t s) {
     const uint32_t L = k + t + 1, N3 = n + 1;
     const uint64_t B = (a.dimension + k - 1) / k;
     if (B == 0 || a.n_vectors == 0) return hipSuccess;
-    const GenTables T = make_gen_tables(L, N3, p, omega_secrets, omega_shares);
+    const uint32_t kv[5] = {L, N3, p, omega_secrets, omega_shares};
+    std::vector<uint8_t> key((const uint8_t*)kv, (const uint8_t*)kv + sizeof(kv));
+    if (tab.key != key) {
+        const GenTables T = make_gen_tables(L, N3, p, omega_secrets, omega_shares);
+        hipError_t e = ensure_table(tab, key, &T, sizeof(T));
+        if (e != hipSuccess) return e;
+    }
+    const GenTables* T = static_cast<const GenTables*>(tab.dev);
     switch (N3) {
         case 3: return gen_dispatch_L<3>(L, a, k, t, B, T, s);
         case 9: return gen_dispatch_L<9>(L, a, k, t, B, T, s);
@@ -182,5 +190,28 @@ hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t
     return hipErrorInvalidValue;
 }
 
+hipError_t ensure_table(DeviceTable& t, const std::vector<uint8_t>& key, const void* host, size_t bytes) {
+    if (t.key == key && t.dev) return hipSuccess;
+    hipError_t e;
+    // earlier launches may still read the old contents
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+    if (bytes > t.cap) {
+        if (t.dev) (void)hipFree(t.dev);
+        t.dev = nullptr;
+        t.cap = 0;
+        if ((e = hipMalloc(&t.dev, bytes)) != hipSuccess) return e;
+        t.cap = bytes;
+    }
+    if ((e = hipMemcpy(t.dev, host, bytes, hipMemcpyHostToDevice)) != hipSuccess) return e;
+    t.key = key;
+    return hipSuccess;
+}
+
+void free_table(DeviceTable& t) {
+    if (t.dev) (void)hipFree(t.dev);
+    t.dev = nullptr;
+    t.cap = 0;
+    t.key.clear();
+}
 
 }  // namespace sda

@@ -147,7 +147,6 @@ __global__ __launch_bounds__(256) void packed_reveal_canon_kernel(const int64_t*
 
 }  // namespace
 
-size_t packed_reveal_scratch_bytes(uint32_t, uint32_t) { return TAB_WORDS * sizeof(uint32_t); }
 
 // Host precompute of the per-index-set tables (data independent; same ops as tss).
 static void build_reveal_tables(std::vector<uint32_t>& tab, const uint64_t* indices, uint32_t n_idx, uint32_t k,
@@ -207,22 +206,24 @@ static hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B,
 }
 
 hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indices, uint32_t n_idx, uint32_t k,
-                                uint32_t t, uint32_t n, uint32_t p, uint32_t omega_secrets, uint32_t omega_shares,
-                                int mode, int64_t* scratch_dev, hipStream_t s) {
-    (void)t; (void)n;
+                                uint32_t p, uint32_t omega_secrets, uint32_t omega_shares, int mode,
+                                DeviceTable& tab, hipStream_t s) {
     const uint64_t B = (a.dimension + k - 1) / k;
     if (B == 0 || a.n_vectors == 0) return hipSuccess;
-    static thread_local std::vector<uint32_t> tab;
-    bool dup = false;
-    build_reveal_tables(tab, indices, n_idx, k, p, omega_secrets, omega_shares, mode == 1, &dup);
-    if (mode == 1 && dup) return hipErrorInvalidValue;
-    hipError_t e = hipMemcpyAsync(scratch_dev, tab.data(), TAB_WORDS * sizeof(uint32_t), hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return e;
-    // the host table must stay valid until the copy has consumed it
-    e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return e;
+    std::vector<uint8_t> key(sizeof(uint32_t) * 6 + sizeof(uint64_t) * n_idx);
+    const uint32_t kv[6] = {n_idx, k, p, omega_secrets, omega_shares, (uint32_t)mode};
+    memcpy(key.data(), kv, sizeof(kv));
+    memcpy(key.data() + sizeof(kv), indices, sizeof(uint64_t) * n_idx);
+    if (tab.key != key) {
+        std::vector<uint32_t> host;
+        bool dup = false;
+        build_reveal_tables(host, indices, n_idx, k, p, omega_secrets, omega_shares, mode == 1, &dup);
+        if (mode == 1 && dup) return hipErrorInvalidValue;
+        hipError_t e = ensure_table(tab, key, host.data(), host.size() * sizeof(uint32_t));
+        if (e != hipSuccess) return e;
+    }
     const MontP M = make_mont(p);
-    const uint32_t* dtab = reinterpret_cast<const uint32_t*>(scratch_dev);
+    const uint32_t* dtab = static_cast<const uint32_t*>(tab.dev);
     const uint32_t m = n_idx + 1;
     const uint32_t need = mode == 0 ? m : n_idx;
     if (need <= 8) return reveal_launch<8>(mode, a, B, n_idx, k, dtab, M, s);

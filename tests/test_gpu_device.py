@@ -10,6 +10,7 @@ import pytest
 from sda_amd import schemes as S
 from sda_amd import engine as E
 from sda_amd import synth
+from tests.util import assert_same
 
 pytestmark = pytest.mark.gpu
 
@@ -44,7 +45,7 @@ def test_combine_dev_large(engine, oracle, dim, stride):
     got = out.cpu().numpy()
     cols = np.random.default_rng(dim).choice(dim, 512, replace=False)
     xs = x[:, torch.from_numpy(cols).cuda()].cpu().numpy()
-    assert got[cols].tolist() == oracle.combine(m, xs).tolist()
+    assert_same(got[cols], oracle.combine(m, xs))
     # property: residue equals the column sum mod m
     col_sum = x[:, :dim].sum(dim=0)           # |sum| < N * m < 2^63
     assert (torch.remainder(col_sum, m).cpu().numpy() == np.mod(got, m)).all()
@@ -90,7 +91,7 @@ def test_packed_dev_roundtrip_config(engine, oracle, mode):
     sec_h, dr_h, sh_h = sec.cpu().numpy(), draws.cpu().numpy(), shares.cpu().numpy()
     for v, b in zip(np.random.default_rng(1).integers(0, V, 64), np.random.default_rng(2).integers(0, B, 64)):
         exp = oracle.packed_share(pp, sec_h[v, b * k:(b + 1) * k], dr_h[v, b])
-        assert sh_h[v, :, b].tolist() == exp.tolist()
+        assert_same(sh_h[v, :, b], exp)
     # reveal from a t+k subset (reversed) and from all clerks: round trip to the secrets
     for idx in (list(range(n - 1, n - 1 - (t + k), -1)), list(range(n))):
         sub = shares[:, idx, :].contiguous()
@@ -105,7 +106,7 @@ def test_packed_dev_roundtrip_config(engine, oracle, mode):
             # exact representatives on a batch sample
             for v, b in zip(range(V), (5, B // 2, B - 1)):
                 rc, exp = oracle.packed_reconstruct(pp, k, idx, sh_h[v][idx][:, b:b + 1])
-                assert got[v, b * k:(b + 1) * k].tolist() == exp.tolist()
+                assert_same(got[v, b * k:(b + 1) * k], exp)
 
 
 def test_chacha_combine_dev(engine, oracle):
@@ -115,7 +116,7 @@ def test_chacha_combine_dev(engine, oracle):
     sd = _dev(seeds.view(np.int32)).view(torch.int32)
     engine.chacha_mask_combine_dev(m, D, sd.data_ptr(), 4, N, out.data_ptr(), _stream())
     torch.cuda.synchronize()
-    assert out.cpu().numpy().tolist() == oracle.chacha_mask_combine(m, D, seeds.astype(np.int64)).tolist()
+    assert_same(out.cpu().numpy(), oracle.chacha_mask_combine(m, D, seeds.astype(np.int64)))
 
 
 def test_additive_generate_dev(engine, oracle):

@@ -4,6 +4,7 @@ Bar: bit-exact (integer work).  Sizes are ones the oracle finishes in seconds; t
 configurations are covered by size-independent properties in test_gpu_device.py.
 """
 import json
+import math
 import os
 
 import numpy as np
@@ -12,6 +13,7 @@ import pytest
 from sda_amd import SdaError, schemes as S
 from sda_amd import engine as E
 from tests.oracle_backend import OracleBackend
+from tests.util import assert_same
 from tests.pipeline import (FULL_LOOP_EXPECTED, FULL_LOOP_INPUTS, README_EXPECTED, README_INPUTS, Draws,
                             full_loop_variants, run_aggregation)
 
@@ -54,7 +56,7 @@ def test_full_loop_kat_many_draws(engine, oracle, variant):
     for seed in range(4):
         a = run_aggregation(engine, masking, sharing, 433, 4, FULL_LOOP_INPUTS, Draws(seed))
         b = run_aggregation(OracleBackend(), masking, sharing, 433, 4, FULL_LOOP_INPUTS, Draws(seed))
-        assert a.masked_output.tolist() == b.masked_output.tolist()
+        assert_same(a.masked_output, b.masked_output)
         assert a.positive.tolist() == FULL_LOOP_EXPECTED
 
 
@@ -63,7 +65,7 @@ def test_full_loop_packed_subsets(engine, oracle):
     for order in ([0, 2, 3, 4, 5, 6, 7], [7, 6, 5, 4, 3, 1, 0], [1, 2, 3, 4, 5, 6, 7]):
         a = run_aggregation(engine, masking, sharing, 433, 4, FULL_LOOP_INPUTS, Draws(7), clerk_order=order)
         b = run_aggregation(OracleBackend(), masking, sharing, 433, 4, FULL_LOOP_INPUTS, Draws(7), clerk_order=order)
-        assert a.masked_output.tolist() == b.masked_output.tolist()
+        assert_same(a.masked_output, b.masked_output)
         assert a.positive.tolist() == FULL_LOOP_EXPECTED
 
 
@@ -93,12 +95,12 @@ def test_combine_random(engine, oracle, m, N, D):
         else:
             x = rng.integers(I64_MIN, I64_MAX, size=(N, D), dtype=np.int64, endpoint=True)
         got = engine.share_combine(S.Additive(3, m), list(x))
-        assert got.tolist() == oracle.combine(m, x).tolist(), kind
+        assert_same(got, oracle.combine(m, x), kind)
 
 
 def test_combine_negative_modulus_and_errors(engine, oracle):
     x = np.array([[5, -7, 12], [9, 3, -20]], np.int64)
-    assert engine.share_combine(S.Additive(3, -10), list(x)).tolist() == oracle.combine(-10, x).tolist()
+    assert_same(engine.share_combine(S.Additive(3, -10), list(x)), oracle.combine(-10, x))
     assert engine.share_combine(S.Additive(3, 433), []).tolist() == []
     with pytest.raises(SdaError) as ei:
         engine.share_combine(S.Additive(3, 433), [[1, 2], [3]])
@@ -111,7 +113,7 @@ def test_combine_negative_modulus_and_errors(engine, oracle):
 def test_additive_reconstruct_is_combine(engine, oracle):
     rows = [np.array([1, -2, 400]), np.array([432, 5, 100]), np.array([-431, 0, -1])]
     got = engine.secret_reconstruct(S.Additive(3, 433), 3, [(2, rows[0]), (0, rows[1]), (1, rows[2])])
-    assert got.tolist() == oracle.combine(433, np.stack(rows)).tolist()
+    assert_same(got, oracle.combine(433, np.stack(rows)))
     with pytest.raises(SdaError) as ei:
         engine.secret_reconstruct(S.Additive(3, 433), 3, [(0, [1, 2]), (1, [1])])
     assert ei.value.status == E.ERR_MISMATCHING_DIMENSION
@@ -133,7 +135,7 @@ def test_additive_generate_random(engine, oracle, n, m):
     secrets[: D // 2] = rng.integers(-(m - 1), m, size=D // 2, dtype=np.int64)
     draws = rng.integers(0, m, size=D * (n - 1), dtype=np.int64)
     got = engine.share_generate(S.Additive(n, m), secrets, draws)
-    assert got.tolist() == oracle.additive_generate(m, n, secrets, draws).tolist()
+    assert_same(got, oracle.additive_generate(m, n, secrets, draws))
 
 
 # ------------------------------------------------------------------ packed Shamir (north-star kernel 2)
@@ -152,7 +154,7 @@ def _roots(p, L, N3):
 
 
 def _prime_for(L, N3, below=2**31):
-    step = L * N3 // np.gcd(L, N3)
+    step = L * N3 // math.gcd(L, N3)
     c = (below - 1) // step
     while True:
         p = c * step + 1
@@ -163,7 +165,7 @@ def _prime_for(L, N3, below=2**31):
 
 def packed_schemes():
     out = [S.FULL_LOOP_PACKED, S.CONFIG_PACKED]
-    for k, t, n in [(1, 0, 2), (3, 4, 26), (7, 8, 26), (1, 1, 8), (15, 16, 80), (8, 7, 80), (31, 32, 80)]:
+    for k, t, n in [(1, 0, 2), (3, 4, 26), (7, 8, 26), (1, 2, 8), (15, 16, 80), (8, 7, 80), (31, 32, 80)]:
         L, N3 = k + t + 1, n + 1
         p = _prime_for(L, N3) if (L, N3) != (8, 27) else 433
         ws, wn = _roots(p, L, N3)
@@ -193,12 +195,12 @@ def test_packed_generate_random(engine, oracle, sch):
     draws = rng.integers(0, p - 1, size=B * sch.privacy_threshold(), dtype=np.int64)
     got = engine.share_generate(sch, secrets, draws)
     exp = oracle.packed_generate(_pp(oracle, sch), secrets, draws)
-    assert got.tolist() == exp.tolist()
+    assert_same(got, exp)
     # raw i64 secrets outside (-p, p): generic exact path (wrapping i64, tss order)
     wide = secrets.copy()
     wide[::5] = rng.integers(-(2**40), 2**40, size=wide[::5].size, dtype=np.int64)
     got = engine.share_generate(sch, wide, draws)
-    assert got.tolist() == oracle.packed_generate(_pp(oracle, sch), wide, draws).tolist()
+    assert_same(got, oracle.packed_generate(_pp(oracle, sch), wide, draws))
 
 
 @pytest.mark.parametrize("sch", packed_schemes(), ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")
@@ -221,7 +223,7 @@ def test_packed_reconstruct_random(engine, oracle, sch):
         got = engine.secret_reconstruct(sch, D, [(i, shares[i]) for i in idx])
         rc, exp = oracle.packed_reconstruct(_pp(oracle, sch), D, idx, shares[idx])
         assert rc == 0
-        assert got.tolist() == exp.tolist()
+        assert_same(got, exp)
         assert (got % p == secrets % p).all()
     # shares outside (-p, p) (e.g. combined shares fed in raw): generic exact path
     idx = list(range(need))
@@ -229,7 +231,7 @@ def test_packed_reconstruct_random(engine, oracle, sch):
     raw[0, ::3] += 5 * p
     got = engine.secret_reconstruct(sch, D, [(i, raw[j]) for j, i in enumerate(idx)])
     rc, exp = oracle.packed_reconstruct(_pp(oracle, sch), D, idx, raw)
-    assert got.tolist() == exp.tolist()
+    assert_same(got, exp)
 
 
 def test_packed_errors(engine):
@@ -255,12 +257,12 @@ def test_chacha_mask_and_combine(engine, oracle, m, words):
     seeds = [rng.integers(0, 2**32, size=words, dtype=np.uint64).astype(np.uint32) for _ in range(5)]
     for sd in seeds[:2]:
         mask, masked = engine.secret_mask(sch, secrets, seed=sd)
-        assert mask.tolist() == sd.astype(np.int64).tolist()
-        assert masked.tolist() == oracle.chacha_mask(m, sd, secrets).tolist()
+        assert_same(mask, sd.astype(np.int64))
+        assert_same(masked, oracle.chacha_mask(m, sd, secrets))
     rows = [sd.astype(np.int64) for sd in seeds]
     got = engine.mask_combine(sch, rows)
     exp = oracle.chacha_mask_combine(m, D, np.stack(rows) if words else np.zeros((5, 0), np.int64))
-    assert got.tolist() == exp.tolist()
+    assert_same(got, exp)
 
 
 def test_chacha_many_seeds(engine, oracle):
@@ -268,7 +270,7 @@ def test_chacha_many_seeds(engine, oracle):
     rng = np.random.default_rng(5)
     rows = [rng.integers(0, 2**32, size=4, dtype=np.uint64).astype(np.int64) for _ in range(N)]
     got = engine.mask_combine(S.ChaChaMasking(m, D, 128), rows)
-    assert got.tolist() == oracle.chacha_mask_combine(m, D, np.stack(rows)).tolist()
+    assert_same(got, oracle.chacha_mask_combine(m, D, np.stack(rows)))
 
 
 def test_chacha_ragged_seed_lengths(engine, oracle):
@@ -278,7 +280,7 @@ def test_chacha_ragged_seed_lengths(engine, oracle):
     padded = np.zeros((4, 4), np.int64)
     for i, r in enumerate(rows):
         padded[i, : len(r)] = r
-    assert got.tolist() == oracle.chacha_mask_combine(m, D, padded).tolist()
+    assert_same(got, oracle.chacha_mask_combine(m, D, padded))
 
 
 def test_chacha_dimension_assert(engine):
@@ -294,13 +296,13 @@ def test_full_mask_unmask_positive(engine, oracle, m):
     secrets = rng.integers(I64_MIN // 2, I64_MAX // 2, size=D, dtype=np.int64)
     masks = rng.integers(0, m, size=D, dtype=np.int64)
     mk, masked = engine.secret_mask(S.FullMasking(m), secrets, full_masks=masks)
-    assert mk.tolist() == masks.tolist()
-    assert masked.tolist() == oracle.full_mask(m, masks, secrets).tolist()
+    assert_same(mk, masks)
+    assert_same(masked, oracle.full_mask(m, masks, secrets))
     rows = [rng.integers(0, m, size=D, dtype=np.int64) for _ in range(7)]
-    assert engine.mask_combine(S.FullMasking(m), rows).tolist() == oracle.combine(m, np.stack(rows)).tolist()
+    assert_same(engine.mask_combine(S.FullMasking(m), rows), oracle.combine(m, np.stack(rows)))
     un = engine.secret_unmask(S.FullMasking(m), (masks, masked))
-    assert un.tolist() == oracle.unmask(m, masks, masked).tolist()
-    assert engine.positive(m, un).tolist() == oracle.positive(m, un).tolist()
-    assert engine.secret_unmask(S.NoMasking(), ([], secrets)).tolist() == secrets.tolist()
+    assert_same(un, oracle.unmask(m, masks, masked))
+    assert_same(engine.positive(m, un), oracle.positive(m, un))
+    assert_same(engine.secret_unmask(S.NoMasking(), ([], secrets)), secrets)
     with pytest.raises(SdaError):
         engine.secret_unmask(S.FullMasking(m), (masks[:-1], masked))
