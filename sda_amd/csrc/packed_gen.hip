@@ -56,11 +56,21 @@ __device__ __noinline__ void packed_share_generic(const int64_t* __restrict__ se
 
 // radix-2 butterfly on exact representatives in (-p, p):  (u ± w c) % p
 __device__ __forceinline__ void bfly2(int32_t& u, int32_t& c, uint32_t w, uint32_t w_m, const MontP& M) {
-    const int64_t t = (int64_t)w * (int64_t)c;                 // exact product, |t| < p^2
+    // exact product, |t| < p^2; w < p < 2^31 so a signed 32x32 multiply is exact (one v_mad_i64_i32)
+    const int64_t t = (int64_t)(int32_t)w * (int64_t)c;
     const uint32_t tc = mont_mul(w_m, canon32(c, M.p), M);     // t mod p (canonical)
     const uint32_t U = canon32(u, M.p);
     const uint32_t c1 = addmod(U, tc, M.p), c2 = submod(U, tc, M.p);
     const int64_t v1 = (int64_t)u + t, v2 = (int64_t)u - t;    // exact dividends
+    u = trunc_from(c1, v1 < 0, M.p);
+    c = trunc_from(c2, v2 < 0, M.p);
+}
+
+// twiddle index 0 is omega^0 = 1 at every level: (u + c) % p, (u - c) % p, no product
+__device__ __forceinline__ void bfly2_unit(int32_t& u, int32_t& c, const MontP& M) {
+    const uint32_t U = canon32(u, M.p), C = canon32(c, M.p);
+    const uint32_t c1 = addmod(U, C, M.p), c2 = submod(U, C, M.p);
+    const int64_t v1 = (int64_t)u + c, v2 = (int64_t)u - c;
     u = trunc_from(c1, v1 < 0, M.p);
     c = trunc_from(c2, v2 < 0, M.p);
 }
@@ -109,7 +119,10 @@ __global__ __launch_bounds__(256) void packed_gen_kernel(const int64_t* __restri
     static_for<1, LB + 1>([&](auto s) {
         constexpr int H = 1 << (s - 1), LEN = 2 * H;
         static_for<0, L, LEN>([&](auto g) {
-            static_for<0, H>([&](auto i) { bfly2(x[g + i], x[g + i + H], T.tw2[H - 1 + i], T.tw2_m[H - 1 + i], T.M); });
+            static_for<0, H>([&](auto i) {
+                if constexpr (i == 0) bfly2_unit(x[g], x[g + H], T.M);
+                else bfly2(x[g + i], x[g + i + H], T.tw2[H - 1 + i], T.tw2_m[H - 1 + i], T.M);
+            });
         });
     });
     // x * len_inv % p   (len_inv > 0 => sign of x)
@@ -128,12 +141,19 @@ __global__ __launch_bounds__(256) void packed_gen_kernel(const int64_t* __restri
                 int32_t r[3];
                 static_for<0, 3>([&](auto q) {
                     constexpr int j = i + q * th;
-                    const uint32_t xw = T.tw3[OB + j], x2 = T.sq3[OB + j];
-                    // exact dividend b + x*c + x^2*d   (|.| < p + 2 p^2 < 2^63)
-                    const int64_t v = (int64_t)bb + (int64_t)xw * cc + (int64_t)x2 * dd;
-                    // canonical residue: REDC(x' C + x2' D) + B    (x' C + x2' D < 2 p^2 < p R)
-                    const uint64_t acc = (uint64_t)T.tw3_m[OB + j] * Cc + (uint64_t)T.sq3_m[OB + j] * Dc;
-                    r[q] = trunc_from(addmod(Bc, redc(acc, T.M), p), v < 0, p);
+                    if constexpr (j == 0) {
+                        // x = x^2 = 1: (b + c + d) % p
+                        const int64_t v = (int64_t)bb + cc + dd;
+                        r[q] = trunc_from(addmod(addmod(Bc, Cc, p), Dc, p), v < 0, p);
+                    } else {
+                        // twiddles < p < 2^31: signed 32x32 products are exact (v_mad_i64_i32)
+                        const int32_t xw = (int32_t)T.tw3[OB + j], x2 = (int32_t)T.sq3[OB + j];
+                        // exact dividend b + x*c + x^2*d   (|.| < p + 2 p^2 < 2^63)
+                        const int64_t v = (int64_t)bb + (int64_t)xw * cc + (int64_t)x2 * dd;
+                        // canonical residue: REDC(x' C + x2' D) + B    (x' C + x2' D < 2 p^2 < p R)
+                        const uint64_t acc = (uint64_t)T.tw3_m[OB + j] * Cc + (uint64_t)T.sq3_m[OB + j] * Dc;
+                        r[q] = trunc_from(addmod(Bc, redc(acc, T.M), p), v < 0, p);
+                    }
                 });
                 y[g + i] = r[0]; y[g + i + th] = r[1]; y[g + i + 2 * th] = r[2];
             });

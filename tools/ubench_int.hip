@@ -1,68 +1,68 @@
 // ubench_int.hip -- issue rates of the integer VALU ops the sharing kernels are built from (gfx950).
-// Each lane runs 8 independent dependency chains of one op; we report lane-ops/s across the chip.
+// Inline asm keeps exactly one instruction per statement; 8 independent chains per lane, full grid.
 //   hipcc -O3 --offload-arch=gfx950 tools/ubench_int.hip -o tools/ubench_int && ./tools/ubench_int
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 
-#define CHAINS 8
-#define ITERS 4096
+#define ITERS 2048
+
+#define REP8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 
 template <int OP>
 __global__ __launch_bounds__(256) void ubench(uint32_t seed, uint64_t* sink) {
-    uint32_t a[CHAINS];
-    uint64_t w[CHAINS];
-    const uint32_t b = seed * 2654435761u + threadIdx.x;
-#pragma unroll
-    for (int c = 0; c < CHAINS; ++c) { a[c] = seed + c * 977 + threadIdx.x; w[c] = a[c]; }
+    uint32_t a0 = seed + threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 * 11, a5 = a0 * 13,
+             a6 = a0 * 17, a7 = a0 * 19;
+    uint64_t w0 = a0, w1 = a1, w2 = a2, w3 = a3, w4 = a4, w5 = a5, w6 = a6, w7 = a7;
+    uint32_t b = seed * 2654435761u + threadIdx.x;
     for (int it = 0; it < ITERS; ++it) {
-#pragma unroll
-        for (int c = 0; c < CHAINS; ++c) {
-            if constexpr (OP == 0) a[c] = a[c] + b;                                   // v_add_u32
-            if constexpr (OP == 1) a[c] = a[c] * b;                                   // v_mul_lo_u32
-            if constexpr (OP == 2) a[c] = __umulhi(a[c], b) ^ c;                      // v_mul_hi_u32 (+xor)
-            if constexpr (OP == 3) w[c] = (uint64_t)(uint32_t)w[c] * b + w[c];        // v_mad_u64_u32
-            if constexpr (OP == 4) w[c] = (uint64_t)((int64_t)(int32_t)w[c] * (int32_t)b + (int64_t)w[c]);  // v_mad_i64_i32
-            if constexpr (OP == 5) a[c] = __builtin_amdgcn_alignbit(a[c], a[c], 7) ^ b;   // rotate + xor
-            if constexpr (OP == 6) w[c] = w[c] + (uint64_t)b;                        // 64-bit add (2 ops)
-            if constexpr (OP == 7) { double d = (double)a[c]; a[c] = (uint32_t)(d * 1.0000001 + 3.0); } // f64 fma + cvts
-        }
+#define STEP(i)                                                                                         \
+        if constexpr (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a##i) : "v"(b));             \
+        if constexpr (OP == 1) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a##i) : "v"(b));          \
+        if constexpr (OP == 2) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a##i) : "v"(b));          \
+        if constexpr (OP == 3) asm volatile("v_mad_u64_u32 %0, s[40:41], %1, %2, %0" : "+v"(w##i) : "v"(b), "v"(b) : "s40", "s41"); \
+        if constexpr (OP == 4) asm volatile("v_mad_i64_i32 %0, s[40:41], %1, %2, %0" : "+v"(w##i) : "v"(b), "v"(b) : "s40", "s41"); \
+        if constexpr (OP == 5) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(a##i));                \
+        if constexpr (OP == 6) asm volatile("v_min_u32 %0, %0, %1" : "+v"(a##i) : "v"(b));             \
+        if constexpr (OP == 7) asm volatile("v_cmp_gt_u32 vcc, %0, %1\n\tv_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##i) : "v"(b) : "vcc"); \
+        if constexpr (OP == 8) asm volatile("v_lshl_add_u64 %0, %0, 1, %0" : "+v"(w##i));              \
+        if constexpr (OP == 9) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a##i) : "v"(b));
+        REP8(STEP)
     }
-    uint64_t s = 0;
-#pragma unroll
-    for (int c = 0; c < CHAINS; ++c) s += a[c] + w[c];
+    uint64_t s = (uint64_t)a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + w0 + w1 + w2 + w3 + w4 + w5 + w6 + w7;
     if (s == 0x12345) sink[threadIdx.x] = s;
 }
 
 template <int OP>
-double run(const char* name, uint64_t* sink) {
+void run(const char* name, uint64_t* sink, int insts_per_step) {
     hipEvent_t e0, e1;
-    hipEventCreate(&e0); hipEventCreate(&e1);
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
     const int blocks = 256 * 8;
     hipLaunchKernelGGL(ubench<OP>, dim3(blocks), dim3(256), 0, 0, 1u, sink);
-    hipEventRecord(e0);
+    (void)hipEventRecord(e0);
     for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(ubench<OP>, dim3(blocks), dim3(256), 0, 0, (uint32_t)r + 2, sink);
-    hipEventRecord(e1);
-    hipEventSynchronize(e1);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
     float ms = 0;
-    hipEventElapsedTime(&ms, e0, e1);
-    const double ops = 5.0 * blocks * 256.0 * ITERS * CHAINS;
-    const double rate = ops / (ms * 1e-3);
-    printf("%-28s %8.2f T lane-ops/s  (%.3f ms/launch)\n", name, rate / 1e12, ms / 5);
-    return rate;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    const double insts = 5.0 * blocks * 256.0 * ITERS * 8 * insts_per_step;
+    printf("%-22s %7.2f T lane-instr/s  (%.3f ms/launch)\n", name, insts / (ms * 1e-3) / 1e12, ms / 5);
 }
 
 int main() {
     uint64_t* sink;
-    hipMalloc(&sink, 4096);
-    run<0>("v_add_u32", sink);
-    run<1>("v_mul_lo_u32", sink);
-    run<2>("v_mul_hi_u32 + xor", sink);
-    run<3>("v_mad_u64_u32", sink);
-    run<4>("v_mad_i64_i32", sink);
-    run<5>("v_alignbit + xor", sink);
-    run<6>("u64 add (2 ops)", sink);
-    run<7>("f64 cvt+fma+cvt", sink);
-    hipFree(sink);
+    (void)hipMalloc(&sink, 4096);
+    run<0>("v_add_u32", sink, 1);
+    run<9>("v_xor_b32", sink, 1);
+    run<6>("v_min_u32", sink, 1);
+    run<5>("v_alignbit_b32", sink, 1);
+    run<7>("v_cmp + v_cndmask", sink, 2);
+    run<1>("v_mul_lo_u32", sink, 1);
+    run<2>("v_mul_hi_u32", sink, 1);
+    run<3>("v_mad_u64_u32", sink, 1);
+    run<4>("v_mad_i64_i32", sink, 1);
+    run<8>("v_lshl_add_u64", sink, 1);
+    (void)hipFree(sink);
     return 0;
 }
