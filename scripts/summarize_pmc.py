@@ -1,0 +1,18 @@
+"""Average each PMC counter per kernel over a rocprofv3 --pmc output directory."""
+import collections
+import csv
+import glob
+import sys
+
+rows = []
+for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
+    rows += list(csv.DictReader(open(f)))
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for r in rows:
+    name = r.get("Kernel_Name", "?")
+    short = name.replace("(anonymous namespace)::", "").split("(")[0][:90]
+    acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, cs in acc.items():
+    print(k)
+    for c, v in sorted(cs.items()):
+        print(f"   {c:28s} {sum(v)/len(v):16.4g}   (n={len(v)})")

@@ -119,6 +119,29 @@ __device__ __forceinline__ int32_t trunc_from(uint32_t c, bool neg, uint32_t p) 
     return neg ? (c ? (int32_t)c - (int32_t)p : 0) : (int32_t)c;
 }
 
+// ---------------------------------------------------------------------------------------
+// Compare-free variants (no VCC write => no VALU->lane-mask hazard s_nops on gfx950).
+// ---------------------------------------------------------------------------------------
+// [0, 2p) -> [0, p):  t - p wraps above t when t < p, so the unsigned min picks the residue.
+__device__ __forceinline__ uint32_t red1(uint32_t t, uint32_t p) { return min(t, t - p); }
+__device__ __forceinline__ uint32_t addm(uint32_t a, uint32_t b, uint32_t p) { return red1(a + b, p); }
+__device__ __forceinline__ uint32_t subm(uint32_t a, uint32_t b, uint32_t p) {
+    const uint32_t d = a - b;            // a < b: wraps to >= 2^32 - p > d + p
+    return min(d, d + p);
+}
+// REDC without the final subtraction: T < p * 2^32  ->  [0, 2p), congruent to T * 2^-32.
+__device__ __forceinline__ uint32_t redc_lazy(uint64_t T, const MontP& M) {
+    const uint32_t u = (uint32_t)T * M.pinv;
+    return (uint32_t)((T + (uint64_t)u * M.p) >> 32);   // T + u p < 2^63 + 2^63
+}
+// Rust `v % p` from the canonical residue c of v and a word whose bit 31 is the sign of v:
+// c - p when v < 0 and c != 0, else c  (sign bit of (sw & -c) is exactly that condition).
+__device__ __forceinline__ int32_t trunc_rep(uint32_t c, uint32_t sw, uint32_t p) {
+    const int32_t m = (int32_t)(sw & (0u - c)) >> 31;
+    return (int32_t)(c - (p & (uint32_t)m));
+}
+__device__ __forceinline__ uint32_t hi32(int64_t v) { return (uint32_t)((uint64_t)v >> 32); }
+
 // (a + b) mod p for canonical a, b
 __device__ __forceinline__ uint32_t addmod(uint32_t a, uint32_t b, uint32_t p) {
     uint32_t s = a + b;          // < 2p < 2^32

@@ -54,58 +54,129 @@ __device__ __noinline__ void packed_share_generic(const int64_t* __restrict__ se
     for (int j = 1; j < N3; ++j) o[(uint64_t)(j - 1) * B] = y[j];
 }
 
-// radix-2 butterfly on exact representatives in (-p, p):  (u ± w c) % p
-__device__ __forceinline__ void bfly2(int32_t& u, int32_t& c, uint32_t w, uint32_t w_m, const MontP& M) {
-    // exact product, |t| < p^2; w < p < 2^31 so a signed 32x32 multiply is exact (one v_mad_i64_i32)
-    const int64_t t = (int64_t)(int32_t)w * (int64_t)c;
-    const uint32_t tc = mont_mul(w_m, canon32(c, M.p), M);     // t mod p (canonical)
-    const uint32_t U = canon32(u, M.p);
-    const uint32_t c1 = addmod(U, tc, M.p), c2 = submod(U, tc, M.p);
-    const int64_t v1 = (int64_t)u + t, v2 = (int64_t)u - t;    // exact dividends
-    u = trunc_from(c1, v1 < 0, M.p);
-    c = trunc_from(c2, v2 < 0, M.p);
+// A field element on the fast path: tss' exact representative s in (-p, p) and its canonical
+// residue c in [0, p).  Carrying both saves re-canonicalising every operand at every stage.
+struct FE {
+    int32_t s;
+    uint32_t c;
+};
+
+// radix-2 butterfly (u ± w c) % p.  The signs come from the exact i64 dividends (one
+// v_mad_i64_i32 each), the residues from one lazy Montgomery product shared by both outputs.
+__device__ __forceinline__ void bfly2(FE& u, FE& c, int32_t w, int32_t nw, uint32_t w_m, const MontP& M) {
+    const int64_t v1 = (int64_t)u.s + (int64_t)w * c.s;
+    const int64_t v2 = (int64_t)u.s + (int64_t)nw * c.s;
+    const uint32_t tc = red1(redc_lazy((uint64_t)w_m * c.c, M), M.p);
+    const uint32_t c1 = addm(u.c, tc, M.p), c2 = subm(u.c, tc, M.p);
+    u = FE{trunc_rep(c1, hi32(v1), M.p), c1};
+    c = FE{trunc_rep(c2, hi32(v2), M.p), c2};
 }
 
-// twiddle index 0 is omega^0 = 1 at every level: (u + c) % p, (u - c) % p, no product
-__device__ __forceinline__ void bfly2_unit(int32_t& u, int32_t& c, const MontP& M) {
-    const uint32_t U = canon32(u, M.p), C = canon32(c, M.p);
-    const uint32_t c1 = addmod(U, C, M.p), c2 = submod(U, C, M.p);
-    const int64_t v1 = (int64_t)u + c, v2 = (int64_t)u - c;
-    u = trunc_from(c1, v1 < 0, M.p);
-    c = trunc_from(c2, v2 < 0, M.p);
+// twiddle omega^0 = 1: (u + c) % p, (u - c) % p.  A saturating add keeps the exact sum's sign.
+__device__ __forceinline__ void bfly2_unit(FE& u, FE& c, uint32_t p) {
+    const uint32_t c1 = addm(u.c, c.c, p), c2 = subm(u.c, c.c, p);
+    const int32_t s1 = __builtin_elementwise_add_sat(u.s, c.s), s2 = __builtin_elementwise_sub_sat(u.s, c.s);
+    u = FE{trunc_rep(c1, (uint32_t)s1, p), c1};
+    c = FE{trunc_rep(c2, (uint32_t)s2, p), c2};
 }
+
+// Compile-time map of the radix-3 registers that hold a known zero (the zero padding of
+// coefficients L..N3-1) after `stage` levels: a group whose c and d are zero just copies b.
+template <int L, int N3>
+struct Zero3 {
+    static constexpr int ND = ilog(N3, 3);
+    static constexpr bool is_zero(int stage, int pos) {
+        if (stage == 0) return rev_digits(pos, 3, ND) >= L;
+        const int th = ipow(3, stage - 1), len = 3 * th;
+        const int g = pos - pos % len, i = (pos % len) % th;
+        return is_zero(stage - 1, g + i) && is_zero(stage - 1, g + i + th) && is_zero(stage - 1, g + i + 2 * th);
+    }
+};
+
+// Workgroup size: 256 batches, fewer for the wide transforms so the LDS stage stays <= 32 KiB.
+template <int L>
+constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
+
+#ifndef SDA_GEN_WAVES
+#define SDA_GEN_WAVES 4
+#endif
 
 template <int L, int N3>
-__global__ __launch_bounds__(256) void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D,
-                                                         const int64_t* __restrict__ draws,
-                                                         int64_t* __restrict__ out, uint32_t k, uint32_t t,
-                                                         uint64_t B, const GenTables* __restrict__ Tp) {
+__global__ __launch_bounds__(gen_block<L>()) __attribute__((amdgpu_waves_per_eu(SDA_GEN_WAVES)))
+void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const int64_t* __restrict__ draws,
+                       int64_t* __restrict__ out, uint32_t k, uint32_t t, uint64_t B,
+                       const GenTables* __restrict__ Tp) {
     const GenTables& T = *Tp;          // global memory: uniform => scalar loads, no per-lane copy
     constexpr int LB = ilog(L, 2);
     constexpr int ND = ilog(N3, 3);
-    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+    constexpr int BS = gen_block<L>();
+    using Z = Zero3<L, N3>;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * BS;
+    const uint64_t b = b0 + tid;
     const uint64_t vec = blockIdx.y;
     const int64_t* sec = secrets + vec * D;
     const int64_t* drw = draws + (vec * B + b) * t;
-    const uint32_t p = T.M.p;
+    const MontP M = T.M;
+    const uint32_t p = M.p;
     const int64_t P = (int64_t)p;
 
-    // values = [0, secrets, randomness]; batched.rs:37-43 zero-pads the tail batch
+    // ---- stage this workgroup's inputs through LDS with coalesced loads ----
+    // lds[0, BS k): the secrets of batches b0.. (zero past D: batched.rs:37-43 pads the tail
+    // batch); lds[BS k, BS (k + t)): their randomness.  Loads are issued U at a time before
+    // the first wait.
+    __shared__ int64_t lds[BS * (L - 1)];
+    {
+        constexpr int U = 8;
+        const uint64_t nb = B - b0 < (uint64_t)BS ? B - b0 : (uint64_t)BS;
+        const uint64_t s0 = b0 * k;
+        const uint32_t ns = (uint32_t)nb * k;
+        const uint32_t valid = D > s0 ? (uint32_t)(D - s0 < ns ? D - s0 : ns) : 0u;
+        const int64_t* ssrc = sec + s0;
+        for (uint32_t base = 0; base < ns; base += U * BS) {
+            int64_t v[U];
+            static_for<0, U>([&](auto u) {
+                const uint32_t e = base + u * BS + tid;
+                v[u] = ssrc[e < valid ? e : 0];
+            });
+            static_for<0, U>([&](auto u) {
+                const uint32_t e = base + u * BS + tid;
+                if (e < ns) lds[e] = e < valid ? v[u] : 0;
+            });
+        }
+        const uint32_t nd = (uint32_t)nb * t;
+        const int64_t* dsrc = draws + (vec * B + b0) * t;
+        int64_t* ldr = lds + (uint32_t)BS * k;
+        for (uint32_t base = 0; base < nd; base += U * BS) {
+            int64_t v[U];
+            static_for<0, U>([&](auto u) {
+                const uint32_t e = base + u * BS + tid;
+                v[u] = dsrc[e < nd ? e : 0];
+            });
+            static_for<0, U>([&](auto u) {
+                const uint32_t e = base + u * BS + tid;
+                if (e < nd) ldr[e] = v[u];
+            });
+        }
+    }
+    __syncthreads();
+    if (b >= B) return;
+
+    // values = [0, secrets, randomness]
     int64_t raw[L];
     raw[0] = 0;
+    {
+        const int64_t* ls = lds + tid * k - 1;                              // + i,      i <= k
+        const int64_t* ld = lds + (uint32_t)BS * k + tid * t - 1 - k;       // + i,      i >  k
+#if SDA_GEN_EXPERIMENT == 1
+        static_for<1, L>([&](auto i) { raw[i] = (int64_t)((b * 2654435761u + i * 40503u) % p); });
+        (void)ls; (void)ld;
+#else
+        static_for<1, L>([&](auto i) { raw[i] = ((uint32_t)i <= k ? ls : ld)[i]; });
+#endif
+    }
     bool in_range = true;
-    static_for<1, L>([&](auto i) {
-        int64_t v;
-        if ((uint32_t)i <= k) {
-            const uint64_t idx = b * k + (i - 1);
-            v = idx < D ? sec[idx] : 0;
-        } else {
-            v = drw[i - 1 - k];
-        }
-        raw[i] = v;
-        in_range = in_range && (v > -P) && (v < P);
-    });
+    static_for<1, L>([&](auto i) { in_range = in_range && ((uint64_t)(raw[i] + (P - 1)) < (uint64_t)(2 * P - 1)); });
 
     int64_t* o = out + vec * (uint64_t)(N3 - 1) * B + b;
     if (!in_range) {
@@ -114,53 +185,92 @@ __global__ __launch_bounds__(256) void packed_gen_kernel(const int64_t* __restri
     }
 
     // ---- fft2_inverse: radix-2 DIT over omega_secrets^-1 on bit-reversed registers ----
-    int32_t x[L];
-    static_for<0, L>([&](auto i) { x[rev_digits(i, 2, LB)] = (int32_t)raw[i]; });
+    FE x[L];
+    static_for<0, L>([&](auto i) {
+        const int32_t s = (int32_t)raw[i];
+        x[rev_digits(i, 2, LB)] = FE{s, canon32(s, p)};
+    });
     static_for<1, LB + 1>([&](auto s) {
         constexpr int H = 1 << (s - 1), LEN = 2 * H;
         static_for<0, L, LEN>([&](auto g) {
             static_for<0, H>([&](auto i) {
-                if constexpr (i == 0) bfly2_unit(x[g], x[g + H], T.M);
-                else bfly2(x[g + i], x[g + i + H], T.tw2[H - 1 + i], T.tw2_m[H - 1 + i], T.M);
+                if constexpr (i == 0) {
+                    bfly2_unit(x[g], x[g + H], p);
+                } else {
+                    const int32_t w = (int32_t)T.tw2[H - 1 + i];
+                    bfly2(x[g + i], x[g + i + H], w, -w, T.tw2_m[H - 1 + i], M);
+                }
             });
         });
     });
-    // x * len_inv % p   (len_inv > 0 => sign of x)
-    static_for<0, L>([&](auto i) { x[i] = trunc_from(mont_mul(T.linv_m, canon32(x[i], p), T.M), x[i] < 0, p); });
+    // x * len_inv % p   (len_inv > 0 => the exact product has the sign of x)
+    static_for<0, L>([&](auto i) {
+        const uint32_t c = red1(redc_lazy((uint64_t)T.linv_m * x[i].c, M), p);
+        x[i] = FE{trunc_rep(c, (uint32_t)x[i].s, p), c};
+    });
 
     // ---- fft3: radix-3 DIT over omega_shares on digit-reversed, zero-extended registers ----
-    int32_t y[N3];
-    static_for<0, N3>([&](auto i) { y[rev_digits(i, 3, ND)] = i < L ? x[i < L ? (int)i : 0] : 0; });
+    FE y[N3];
+    static_for<0, N3>([&](auto i) {
+        if constexpr (i < L) y[rev_digits(i, 3, ND)] = x[i < L ? (int)i : 0];
+        else y[rev_digits(i, 3, ND)] = FE{0, 0};
+    });
     static_for<1, ND + 1>([&](auto s) {
         constexpr int th = ipow(3, s - 1);
         constexpr int LEN = 3 * th, OB = (LEN - 3) / 2;
+        constexpr bool last = (s == ND);
         static_for<0, N3, LEN>([&](auto g) {
             static_for<0, th>([&](auto i) {
-                const int32_t bb = y[g + i], cc = y[g + i + th], dd = y[g + i + 2 * th];
-                const uint32_t Bc = canon32(bb, p), Cc = canon32(cc, p), Dc = canon32(dd, p);
-                int32_t r[3];
-                static_for<0, 3>([&](auto q) {
-                    constexpr int j = i + q * th;
-                    if constexpr (j == 0) {
-                        // x = x^2 = 1: (b + c + d) % p
-                        const int64_t v = (int64_t)bb + cc + dd;
-                        r[q] = trunc_from(addmod(addmod(Bc, Cc, p), Dc, p), v < 0, p);
-                    } else {
-                        // twiddles < p < 2^31: signed 32x32 products are exact (v_mad_i64_i32)
-                        const int32_t xw = (int32_t)T.tw3[OB + j], x2 = (int32_t)T.sq3[OB + j];
-                        // exact dividend b + x*c + x^2*d   (|.| < p + 2 p^2 < 2^63)
-                        const int64_t v = (int64_t)bb + (int64_t)xw * cc + (int64_t)x2 * dd;
-                        // canonical residue: REDC(x' C + x2' D) + B    (x' C + x2' D < 2 p^2 < p R)
-                        const uint64_t acc = (uint64_t)T.tw3_m[OB + j] * Cc + (uint64_t)T.sq3_m[OB + j] * Dc;
-                        r[q] = trunc_from(addmod(Bc, redc(acc, T.M), p), v < 0, p);
-                    }
-                });
-                y[g + i] = r[0]; y[g + i + th] = r[1]; y[g + i + 2 * th] = r[2];
+                constexpr bool zc = Z::is_zero(s - 1, g + i + th), zd = Z::is_zero(s - 1, g + i + 2 * th);
+                if constexpr (zc && zd) {
+                    // (b + x 0 + x^2 0) % p == b for b in (-p, p): all three outputs are b
+                    y[g + i + th] = y[g + i];
+                    y[g + i + 2 * th] = y[g + i];
+                } else {
+                    const FE bb = y[g + i], cc = y[g + i + th], dd = y[g + i + 2 * th];
+                    FE r[3];
+                    static_for<0, 3>([&](auto q) {
+                        constexpr int j = i + q * th;
+                        if constexpr (last && g + j == 0) {
+                            r[q] = FE{0, 0};            // points[0] is dropped (shares = points[1..])
+                        } else if constexpr (j == 0) {
+                            // x = x^2 = 1: (b + c + d) % p
+                            if constexpr (zd) {
+                                const uint32_t c = addm(bb.c, cc.c, p);
+                                r[q] = FE{trunc_rep(c, (uint32_t)__builtin_elementwise_add_sat(bb.s, cc.s), p), c};
+                            } else {
+                                const int64_t v = (int64_t)bb.s + cc.s + dd.s;
+                                const uint32_t c = addm(addm(bb.c, cc.c, p), dd.c, p);
+                                r[q] = FE{trunc_rep(c, hi32(v), p), c};
+                            }
+                        } else if constexpr (zd) {
+                            const int32_t xw = (int32_t)T.tw3[OB + j];
+                            const int64_t v = (int64_t)bb.s + (int64_t)xw * cc.s;
+                            const uint32_t c = addm(bb.c, red1(redc_lazy((uint64_t)T.tw3_m[OB + j] * cc.c, M), p), p);
+                            r[q] = FE{trunc_rep(c, hi32(v), p), c};
+                        } else {
+                            // twiddles < p < 2^31: signed 32x32 products are exact (v_mad_i64_i32)
+                            const int32_t xw = (int32_t)T.tw3[OB + j], x2 = (int32_t)T.sq3[OB + j];
+                            const int64_t v = (int64_t)bb.s + (int64_t)xw * cc.s + (int64_t)x2 * dd.s;
+                            // residue: REDC(x' C + x2' D) + B    (x' C + x2' D < 2 p^2 < p R)
+                            const uint64_t acc = (uint64_t)T.tw3_m[OB + j] * cc.c + (uint64_t)T.sq3_m[OB + j] * dd.c;
+                            const uint32_t c = addm(bb.c, red1(redc_lazy(acc, M), p), p);
+                            r[q] = FE{trunc_rep(c, hi32(v), p), c};
+                        }
+                    });
+                    y[g + i] = r[0]; y[g + i + th] = r[1]; y[g + i + 2 * th] = r[2];
+                }
             });
         });
     });
     // shares = points[1..=n], clerk-major (batched.rs:46-48)
-    static_for<1, N3>([&](auto j) { o[(uint64_t)(j - 1) * B] = (int64_t)y[j]; });
+#if SDA_GEN_EXPERIMENT == 2
+    int32_t acc = 0;
+    static_for<1, N3>([&](auto j) { acc ^= y[j].s; });
+    if (acc == 0x7fffffff) o[0] = acc;
+#else
+    static_for<1, N3>([&](auto j) { o[(uint64_t)(j - 1) * B] = (int64_t)y[j].s; });
+#endif
 }
 
 }  // namespace
@@ -168,8 +278,9 @@ __global__ __launch_bounds__(256) void packed_gen_kernel(const int64_t* __restri
 template <int L, int N3>
 static hipError_t gen_launch(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
                              hipStream_t s) {
-    dim3 grid((unsigned)((B + 255) / 256), (unsigned)a.n_vectors);
-    hipLaunchKernelGGL((packed_gen_kernel<L, N3>), grid, dim3(256), 0, s, a.secrets, a.dimension, a.draws, a.out,
+    constexpr int BS = gen_block<L>();
+    dim3 grid((unsigned)((B + BS - 1) / BS), (unsigned)a.n_vectors);
+    hipLaunchKernelGGL((packed_gen_kernel<L, N3>), grid, dim3(BS), 0, s, a.secrets, a.dimension, a.draws, a.out,
                        k, t, B, T);
     return hipGetLastError();
 }
@@ -201,12 +312,16 @@ hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t
         if (e != hipSuccess) return e;
     }
     const GenTables* T = static_cast<const GenTables*>(tab.dev);
+#ifdef SDA_ISA_ONLY      // developer switch: one instantiation, for ISA inspection
+    if (L == 16 && N3 == 27) return gen_launch<16, 27>(a, k, t, B, T, s);
+#else
     switch (N3) {
         case 3: return gen_dispatch_L<3>(L, a, k, t, B, T, s);
         case 9: return gen_dispatch_L<9>(L, a, k, t, B, T, s);
         case 27: return gen_dispatch_L<27>(L, a, k, t, B, T, s);
         case 81: return gen_dispatch_L<81>(L, a, k, t, B, T, s);
     }
+#endif
     return hipErrorInvalidValue;
 }
 

@@ -23,7 +23,8 @@ import numpy as np
 
 from . import schemes as S
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsda_engine.so")
+# SDA_ENGINE_LIB: developer override (A/B builds of the same ABI); the default is the in-tree build.
+LIB_PATH = os.environ.get("SDA_ENGINE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsda_engine.so")
 
 OK = 0
 ERR_BATCH_INPUT_WRONG_LENGTH = 1
