@@ -21,16 +21,17 @@ constexpr size_t OFF_INV = 0, OFF_INVM = (size_t)TS * TS, OFF_NP = 2 * (size_t)T
                  OFF_NPM = OFF_NP + (size_t)KMAX * TS, OFF_LAM = OFF_NPM + (size_t)KMAX * TS,
                  TAB_WORDS = OFF_LAM + (size_t)KMAX * TS;
 
-__device__ __forceinline__ int64_t trunc_small(int64_t x, int64_t p) {   // x in (-2p, 2p)
-    x = x >= p ? x - p : x;
-    return x <= -p ? x + p : x;
-}
+// A field element: tss' exact representative s in (-p, p) and its canonical residue c.
+struct FE {
+    int32_t s;
+    uint32_t c;
+};
 
-// generic exact reveal for one batch (inputs outside (-p, p) or m > unrolled sizes)
-// Reads the batch's shares from global memory and writes its secrets (truncated at D) itself.
+// generic exact reveal for one batch (inputs outside (-p, p)).  Reads the batch's shares from
+// global memory and writes its `lim` first secrets to dst[0..lim).
 __device__ __noinline__ void reveal_exact_generic(const int64_t* __restrict__ sh, uint64_t B, uint32_t m, uint32_t k,
                                                   const uint32_t* __restrict__ tab, const MontP& M,
-                                                  int64_t* o, uint64_t b, uint64_t D) {
+                                                  int64_t* dst, uint32_t lim) {
     const Mod64 P = make_mod64((int64_t)M.p);
     int64_t s[TS];
     s[0] = 0;
@@ -40,109 +41,147 @@ __device__ __noinline__ void reveal_exact_generic(const int64_t* __restrict__ sh
             const int64_t cd = trem64(wsub(s[i], s[i - 1]), P);
             s[i] = trem64(wmul(cd, (int64_t)tab[OFF_INV + j * TS + i]), P);
         }
-    for (uint32_t e = 0; e < k; ++e) {
+    for (uint32_t e = 0; e < k && e < lim; ++e) {
         int64_t acc = 0;
         for (uint32_t i = 0; i < m; ++i) {
             const int64_t np = (int64_t)(int32_t)tab[OFF_NP + e * TS + i];
             acc = trem64(wadd(acc, trem64(wmul(s[i], np), P)), P);
         }
-        if (b * k + e < D) o[b * k + e] = acc;
+        dst[e] = acc;
     }
 }
 
-template <int MMAX>
+// The k secrets of a batch are adjacent in `out` (batched.rs:94 appends batch after batch), so a
+// lane's own stores would stride by 8k bytes.  With STAGED the workgroup parks its results in
+// LDS ([lane][k]) and writes the nb*k block back with coalesced stores.
+template <bool STAGED>
+__device__ __forceinline__ void reveal_flush(int64_t* lds_o, int64_t* o, uint64_t b0, uint64_t B, uint64_t D,
+                                             uint32_t k) {
+    if constexpr (STAGED) {
+        __syncthreads();
+        const uint64_t first = b0 * k;
+        const uint64_t last = (b0 + 256 < B ? b0 + 256 : B) * k;
+        const uint32_t cnt = (uint32_t)((last < D ? last : D) - first);
+        for (uint32_t j = threadIdx.x; j < cnt; j += 256) o[first + j] = lds_o[j];
+    }
+}
+
+template <int MMAX, bool STAGED>
 __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t* __restrict__ shares, uint64_t B,
                                                                   uint64_t D, int64_t* __restrict__ out,
                                                                   uint32_t n_idx, uint32_t k,
                                                                   const uint32_t* __restrict__ tab, MontP M) {
-    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+    extern __shared__ int64_t lds_o[];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * 256, b = b0 + tid;
+    const bool live = b < B;
     const uint64_t vec = blockIdx.y;
-    const int64_t* sh = shares + vec * (uint64_t)n_idx * B + b;
+    const int64_t* sh = shares + vec * (uint64_t)n_idx * B + (live ? b : B - 1);
     int64_t* o = out + vec * D;
     const uint32_t p = M.p;
     const int64_t P = (int64_t)p;
     const uint32_t m = n_idx + 1;
+    int64_t* dst = STAGED ? lds_o + tid * k : o + b * k;
+    const uint32_t lim = STAGED ? k : (b * k < D ? (uint32_t)(D - b * k < k ? D - b * k : k) : 0u);
 
-    // gather [clerk][batch] -> [clerk] (batched.rs:83-85); point 1 carries value 0
-    int32_t s[MMAX];
+    // gather [clerk][batch] -> [clerk] (batched.rs:83-85); point 1 carries value 0.  All loads are
+    // issued before the first wait (clamped, branch-free indices).
+    int64_t v[MMAX];
+    static_for<1, MMAX>([&](auto i) { v[i] = sh[(uint64_t)((uint32_t)i < m ? i - 1 : 0) * B]; });
     bool in_range = true;
-    s[0] = 0;
     static_for<1, MMAX>([&](auto i) {
-        int64_t v = 0;
-        if ((uint32_t)i < m) v = sh[(uint64_t)(i - 1) * B];
-        in_range = in_range && (v > -P) && (v < P);
-        s[i] = (int32_t)v;
+        in_range = in_range && ((uint32_t)i >= m || (uint64_t)(v[i] + (P - 1)) < (uint64_t)(2 * P - 1));
     });
     if (!in_range) {
-        reveal_exact_generic(sh, B, m, k, tab, M, o, b, D);
-        return;
-    }
-    // numtheory::compute_newton_coefficients: for j in 1..m { for i in (j..m).rev() { ... } }
-    static_for<1, MMAX>([&](auto j) {
-        if ((uint32_t)j < m) {
-            static_for<0, MMAX - j>([&](auto ii) {
-                constexpr int i = MMAX - 1 - ii;
-                if ((uint32_t)i < m) {
-                    const int64_t cd = trunc_small((int64_t)s[i] - (int64_t)s[i - 1], P);   // (upper - lower) % p
-                    const uint32_t inv = tab[OFF_INV + j * TS + i], inv_m = tab[OFF_INVM + j * TS + i];
-                    const uint32_t c = mont_mul(inv_m, canon32((int32_t)cd, p), M);       // (cd * inv) % p
-                    s[i] = trunc_from(c, (cd < 0) && (inv != 0), p);
-                }
-            });
-        }
-    });
-    // numtheory::newton_evaluate at omega_secrets^e: fold((a + (coef * np) % p) % p)
-    for (uint32_t e = 0; e < k; ++e) {
-        int64_t acc = 0;
-        static_for<0, MMAX>([&](auto i) {
-            if ((uint32_t)i < m) {
-                const int32_t np = (int32_t)tab[OFF_NP + e * TS + i];
-                const uint32_t c = mont_mul(tab[OFF_NPM + e * TS + i], canon32(s[i], p), M);
-                const bool neg = (s[i] != 0) && (np != 0) && ((s[i] < 0) != (np < 0));
-                acc = trunc_small(acc + trunc_from(c, neg, p), P);
+        if (live) reveal_exact_generic(sh, B, m, k, tab, M, dst, lim);
+    } else {
+        FE s[MMAX];
+        s[0] = FE{0, 0};
+        static_for<1, MMAX>([&](auto i) {
+            const int32_t x = (uint32_t)i < m ? (int32_t)v[i] : 0;
+            s[i] = FE{x, canon32(x, p)};
+        });
+        // numtheory::compute_newton_coefficients: for j in 1..m { for i in (j..m).rev() {
+        //   s[i] = (((s[i] - s[i-1]) % p) * inv(points[i] - points[i-j])) % p } }
+        // inv >= 0, so the product has the sign of the exact difference (or is 0).
+        static_for<1, MMAX>([&](auto j) {
+            if ((uint32_t)j < m) {
+                static_for<0, MMAX - j>([&](auto ii) {
+                    constexpr int i = MMAX - 1 - ii;
+                    if ((uint32_t)i < m) {
+                        const uint32_t dc = subm(s[i].c, s[i - 1].c, p);
+                        const int32_t sg = __builtin_elementwise_sub_sat(s[i].s, s[i - 1].s);
+                        const uint32_t fc = red1(redc_lazy((uint64_t)tab[OFF_INVM + j * TS + i] * dc, M), p);
+                        s[i] = FE{trunc_rep(fc, (uint32_t)sg, p), fc};
+                    }
+                });
             }
         });
-        if (b * k + e < D) o[b * k + e] = acc;                                          // batched.rs:94
+        // numtheory::newton_evaluate at omega_secrets^(e+1): fold((a + (coef * np) % p) % p)
+        for (uint32_t e = 0; e < k; ++e) {
+            const uint32_t* np = tab + OFF_NP + e * TS;
+            const uint32_t* npm = tab + OFF_NPM + e * TS;
+            FE acc{0, 0};
+            static_for<0, MMAX>([&](auto i) {
+                if ((uint32_t)i < m) {
+                    const uint32_t tc = red1(redc_lazy((uint64_t)npm[i] * s[i].c, M), p);
+                    const int32_t ts = trunc_rep(tc, (uint32_t)s[i].s ^ np[i], p);   // sign of s * np
+                    const uint32_t ac = addm(acc.c, tc, p);
+                    acc = FE{trunc_rep(ac, (uint32_t)__builtin_elementwise_add_sat(acc.s, ts), p), ac};
+                }
+            });
+            if (e < lim) dst[e] = acc.s;                                                // batched.rs:94
+        }
     }
+    reveal_flush<STAGED>(lds_o, o, b0, B, D, k);
 }
 
-template <int NMAX>
+template <int NMAX, bool STAGED>
 __global__ __launch_bounds__(256) void packed_reveal_canon_kernel(const int64_t* __restrict__ shares, uint64_t B,
                                                                   uint64_t D, int64_t* __restrict__ out,
                                                                   uint32_t n_idx, uint32_t k,
                                                                   const uint32_t* __restrict__ tab, MontP M) {
-    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+    extern __shared__ int64_t lds_o[];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * 256, b = b0 + tid;
+    const bool live = b < B;
     const uint64_t vec = blockIdx.y;
-    const int64_t* sh = shares + vec * (uint64_t)n_idx * B + b;
+    const int64_t* sh = shares + vec * (uint64_t)n_idx * B + (live ? b : B - 1);
     int64_t* o = out + vec * D;
     const uint32_t p = M.p;
     const int64_t P = (int64_t)p;
-    const Mod64 PM = make_mod64(P);
+    int64_t* dst = STAGED ? lds_o + tid * k : o + b * k;
+    const uint32_t lim = STAGED ? k : (b * k < D ? (uint32_t)(D - b * k < k ? D - b * k : k) : 0u);
+
+    int64_t v[NMAX];
+    static_for<0, NMAX>([&](auto i) { v[i] = sh[(uint64_t)((uint32_t)i < n_idx ? i : 0) * B]; });
     uint32_t S[NMAX];
+    bool in_range = true;
     static_for<0, NMAX>([&](auto i) {
-        uint32_t c = 0;
-        if ((uint32_t)i < n_idx) {
-            const int64_t v = sh[(uint64_t)i * B];
-            if ((v > -P) && (v < P)) c = canon32((int32_t)v, p);
-            else { const int64_t r = trem64(v, PM); c = (uint32_t)(r < 0 ? r + P : r); }
-        }
-        S[i] = c;
+        in_range = in_range && ((uint32_t)i >= n_idx || (uint64_t)(v[i] + (P - 1)) < (uint64_t)(2 * P - 1));
+        S[i] = (uint32_t)i < n_idx ? canon32((int32_t)v[i], p) : 0u;
     });
+    if (!in_range) {                    // raw i64 shares: exact canonical residues (rare)
+        const Mod64 PM = make_mod64(P);
+        static_for<0, NMAX>([&](auto i) {
+            const int64_t r = trem64(v[i], PM);
+            S[i] = (uint32_t)i < n_idx ? (uint32_t)(r < 0 ? r + P : r) : 0u;
+        });
+    }
+    // secret_e = sum_i lambda_{e,i} share_i  (mod p); pairs of products share one REDC (2 p^2 < p R)
     for (uint32_t e = 0; e < k; ++e) {
+        const uint32_t* lam = tab + OFF_LAM + e * TS;
         uint32_t acc = 0;
         static_for<0, NMAX, 2>([&](auto i) {
             if ((uint32_t)i < n_idx) {
-                uint64_t T = (uint64_t)tab[OFF_LAM + e * TS + i] * S[i];
-                if constexpr (i + 1 < NMAX) {
-                    if ((uint32_t)(i + 1) < n_idx) T += (uint64_t)tab[OFF_LAM + e * TS + i + 1] * S[i + 1];
-                }
-                acc = addmod(acc, redc(T, M), p);                    // 2 p^2 < p R
+                uint64_t T = (uint64_t)lam[i] * S[i];
+                if constexpr (i + 1 < NMAX) T += (uint64_t)lam[i + 1] * S[i + 1];   // lam, S are 0 past n_idx
+                acc = addm(acc, red1(redc_lazy(T, M), p), p);
             }
         });
-        if (b * k + e < D) o[b * k + e] = (int64_t)acc;
+        if (e < lim) dst[e] = (int64_t)acc;
     }
+    reveal_flush<STAGED>(lds_o, o, b0, B, D, k);
 }
 
 }  // namespace
@@ -196,12 +235,23 @@ template <int MM>
 static hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32_t n_idx, uint32_t k,
                                 const uint32_t* tab, const MontP& M, hipStream_t s) {
     dim3 grid((unsigned)((B + 255) / 256), (unsigned)a.n_vectors);
-    if (mode == 0)
-        hipLaunchKernelGGL((packed_reveal_exact_kernel<MM>), grid, dim3(256), 0, s, a.shares, B, a.dimension, a.out,
-                           n_idx, k, tab, M);
-    else
-        hipLaunchKernelGGL((packed_reveal_canon_kernel<MM>), grid, dim3(256), 0, s, a.shares, B, a.dimension, a.out,
-                           n_idx, k, tab, M);
+    const bool staged = k <= 16;                      // LDS stage: 256 * k * 8 B <= 32 KiB
+    const size_t lds = staged ? (size_t)256 * k * sizeof(int64_t) : 0;
+    if (mode == 0) {
+        if (staged)
+            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true>), grid, dim3(256), lds, s, a.shares, B,
+                               a.dimension, a.out, n_idx, k, tab, M);
+        else
+            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, false>), grid, dim3(256), 0, s, a.shares, B,
+                               a.dimension, a.out, n_idx, k, tab, M);
+    } else {
+        if (staged)
+            hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, true>), grid, dim3(256), lds, s, a.shares, B,
+                               a.dimension, a.out, n_idx, k, tab, M);
+        else
+            hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, false>), grid, dim3(256), 0, s, a.shares, B,
+                               a.dimension, a.out, n_idx, k, tab, M);
+    }
     return hipGetLastError();
 }
 
@@ -226,6 +276,9 @@ hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indic
     const uint32_t* dtab = static_cast<const uint32_t*>(tab.dev);
     const uint32_t m = n_idx + 1;
     const uint32_t need = mode == 0 ? m : n_idx;
+#ifdef SDA_ISA_ONLY      // developer switch: one instantiation, for ISA inspection
+    if (need <= 16) return reveal_launch<16>(mode, a, B, n_idx, k, dtab, M, s);
+#endif
     if (need <= 8) return reveal_launch<8>(mode, a, B, n_idx, k, dtab, M, s);
     if (need <= 16) return reveal_launch<16>(mode, a, B, n_idx, k, dtab, M, s);
     if (need <= 32) return reveal_launch<32>(mode, a, B, n_idx, k, dtab, M, s);
