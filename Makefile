@@ -1,25 +1,40 @@
 # Build for MI355X (gfx950).  `make` builds the engine and the oracle (test infrastructure).
+# The packed-Shamir kernels are compiled as one object per instantiation family
+# (SDA_GEN_PART = n+1, SDA_REVEAL_PART = padded point count) so `make -j` builds them in parallel.
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
-JOBS     ?= 8
+EXTRA    ?=
 
 CSRC    := sda_amd/csrc
-OBJDIR  := build/obj
-SRCS    := $(CSRC)/combine.hip $(CSRC)/elementwise.hip $(CSRC)/packed_gen.hip $(CSRC)/packed_reveal.hip $(CSRC)/chacha.hip
-OBJS    := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS)) $(OBJDIR)/engine.o
+OBJDIR  ?= build/obj
+LIB     ?= sda_amd/libsda_engine.so
+
+GEN_PARTS    := 3 9 27 81
+REVEAL_PARTS := 8 16 32 64
+PLAIN   := combine elementwise chacha
+OBJS    := $(patsubst %,$(OBJDIR)/%.o,$(PLAIN)) $(OBJDIR)/engine.o \
+           $(OBJDIR)/packed_gen.o $(patsubst %,$(OBJDIR)/packed_gen_%.o,$(GEN_PARTS)) \
+           $(OBJDIR)/packed_reveal.o $(patsubst %,$(OBJDIR)/packed_reveal_%.o,$(REVEAL_PARTS))
 HDRS    := $(CSRC)/packed_common.h $(CSRC)/kernels.h $(CSRC)/modarith.h include/sda_engine.h
-LIB     := sda_amd/libsda_engine.so
 
 all: $(LIB) oracle
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(EXTRA) -c $< -o $@
+
+$(OBJDIR)/packed_gen_%.o: $(CSRC)/packed_gen.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(EXTRA) -DSDA_GEN_PART=$* -c $< -o $@
+
+$(OBJDIR)/packed_reveal_%.o: $(CSRC)/packed_reveal.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(EXTRA) -DSDA_REVEAL_PART=$* -c $< -o $@
 
 $(OBJDIR)/engine.o: $(CSRC)/engine.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(EXTRA) -x hip -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
@@ -27,11 +42,8 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
-tests-cpp: $(LIB)
-	$(MAKE) -C tests/cpp
-
 clean:
 	rm -rf build $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean tests-cpp
+.PHONY: all oracle clean

@@ -25,6 +25,8 @@ struct sda_engine {
     void* stage = nullptr;        // staging for host-path inputs/outputs
     size_t stage_bytes = 0;
     sda::DeviceTable gen_tab;     // packed-Shamir twiddles (per scheme)
+    void* gen_log = nullptr;      // packed-Shamir generic fix-up log (sda::packed_gen_log_bytes())
+    size_t gen_log_bytes = 0;
     sda::DeviceTable rev_tab;     // packed-Shamir Newton/Lagrange tables (per scheme + clerk set)
 };
 
@@ -193,6 +195,7 @@ void sda_engine_destroy(sda_engine* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->work) (void)hipFree(h->work);
+    if (h->gen_log) (void)hipFree(h->gen_log);
     if (h->stage) (void)hipFree(h->stage);
     sda::free_table(h->gen_tab);
     sda::free_table(h->rev_tab);
@@ -265,9 +268,10 @@ sda_status sda_share_generate(sda_engine* h, const sda_sharing_scheme* s, const 
     HIP_TRY(hipMemcpyAsync(dsec, secrets, D * 8, hipMemcpyHostToDevice, h->stream));
     if (n_draws) HIP_TRY(hipMemcpyAsync(ddr, draws, n_draws * 8, hipMemcpyHostToDevice, h->stream));
     sda::PackedGenArgs ga{dsec, D, 1, ddr, dout};
+    if (sda_status st = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return st;
     HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)k, (uint32_t)t, (uint32_t)n, (uint32_t)s->modulus,
                                         (uint32_t)s->omega_secrets, (uint32_t)s->omega_shares, h->gen_tab,
-                                        h->stream));
+                                        h->gen_log, h->stream));
     HIP_TRY(hipMemcpyAsync(out, dout, n * B * 8, hipMemcpyDeviceToHost, h->stream));
     return finish(h);
 }
@@ -530,9 +534,10 @@ sda_status sda_packed_generate_dev(sda_engine* h, const sda_sharing_scheme* s, c
     if (n_vectors > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 vectors per launch");
     HIP_TRY(hipSetDevice(h->device));
     sda::PackedGenArgs ga{secrets, dimension, n_vectors, draws, out};
+    if (sda_status st = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return st;
     HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)s->secret_count, (uint32_t)s->privacy_threshold,
                                         (uint32_t)s->share_count, (uint32_t)s->modulus, (uint32_t)s->omega_secrets,
-                                        (uint32_t)s->omega_shares, h->gen_tab, pick(h, stream)));
+                                        (uint32_t)s->omega_shares, h->gen_tab, h->gen_log, pick(h, stream)));
     return ok();
 }
 

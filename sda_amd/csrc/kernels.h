@@ -44,8 +44,18 @@ struct PackedGenArgs {
     const int64_t* secrets; uint64_t dimension; uint64_t n_vectors;
     const int64_t* draws; int64_t* out;
 };
+// Batches whose inputs fall outside (-p, p) are logged by the fast kernel and recomputed by a
+// generic exact fix-up kernel.  `log_buf` is device memory of packed_gen_log_bytes() bytes.
+constexpr uint32_t kGenLogCap = 1u << 16;
+struct GenFixupLog {
+    unsigned int* count;
+    uint64_t* list;        // vec * B + batch
+    uint32_t cap;
+};
+size_t packed_gen_log_bytes();
 hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t, uint32_t n, uint32_t p,
-                                  uint32_t omega_secrets, uint32_t omega_shares, DeviceTable& tab, hipStream_t s);
+                                  uint32_t omega_secrets, uint32_t omega_shares, DeviceTable& tab, void* log_buf,
+                                  hipStream_t s);
 struct PackedRevealArgs {
     const int64_t* shares; uint64_t dimension; uint64_t n_vectors; int64_t* out;
 };

@@ -4,6 +4,300 @@
 namespace sda {
 using namespace packed;
 
+// One dispatcher per N3 = n+1; each is compiled in its own object (Makefile: -DSDA_GEN_PART=N3)
+// so the instantiations build in parallel.
+template <int N3>
+hipError_t gen_dispatch_L(uint32_t L, const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B,
+                          const GenTables* T, const GenFixupLog& log, hipStream_t s);
+
+#ifdef SDA_GEN_PART
+namespace {
+
+// A field element on the fast path: tss' exact representative s in (-p, p) and its canonical
+// residue c in [0, p).  Carrying both saves re-canonicalising every operand at every stage.
+struct FE {
+    int32_t s;
+    uint32_t c;
+};
+
+// radix-2 butterfly (u ± w c) % p.  The signs come from the exact i64 dividends (one
+// v_mad_i64_i32 each), the residues from one lazy Montgomery product shared by both outputs.
+__device__ __forceinline__ void bfly2(FE& u, FE& c, int32_t w, int32_t nw, uint32_t w_m, const MontP& M) {
+    const int64_t v1 = (int64_t)u.s + (int64_t)w * c.s;
+    const int64_t v2 = (int64_t)u.s + (int64_t)nw * c.s;
+    const uint32_t tc = red1(redc_lazy((uint64_t)w_m * c.c, M), M.p);
+    const uint32_t c1 = addm(u.c, tc, M.p), c2 = subm(u.c, tc, M.p);
+    u = FE{trunc_rep(c1, hi32(v1), M.p), c1};
+    c = FE{trunc_rep(c2, hi32(v2), M.p), c2};
+}
+
+// twiddle omega^0 = 1: (u + c) % p, (u - c) % p.  A saturating add keeps the exact sum's sign.
+__device__ __forceinline__ void bfly2_unit(FE& u, FE& c, uint32_t p) {
+    const uint32_t c1 = addm(u.c, c.c, p), c2 = subm(u.c, c.c, p);
+    const int32_t s1 = __builtin_elementwise_add_sat(u.s, c.s), s2 = __builtin_elementwise_sub_sat(u.s, c.s);
+    u = FE{trunc_rep(c1, (uint32_t)s1, p), c1};
+    c = FE{trunc_rep(c2, (uint32_t)s2, p), c2};
+}
+
+// Compile-time map of the radix-3 registers that hold a known zero (the zero padding of
+// coefficients L..N3-1) after `stage` levels: a group whose c and d are zero just copies b.
+template <int L, int N3>
+struct Zero3 {
+    static constexpr int ND = ilog(N3, 3);
+    static constexpr bool is_zero(int stage, int pos) {
+        if (stage == 0) return rev_digits(pos, 3, ND) >= L;
+        const int th = ipow(3, stage - 1), len = 3 * th;
+        const int g = pos - pos % len, i = (pos % len) % th;
+        return is_zero(stage - 1, g + i) && is_zero(stage - 1, g + i + th) && is_zero(stage - 1, g + i + 2 * th);
+    }
+};
+
+// Workgroup size: 256 batches, fewer for the wide transforms so the LDS stage stays <= 32 KiB.
+template <int L>
+constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
+
+#ifndef SDA_GEN_WAVES
+#define SDA_GEN_WAVES 4
+#endif
+
+
+// One workgroup = one tile (vector blockIdx.y, BS batches from blockIdx.x * BS).
+//
+// Lane -> batch map: lane i < 32 takes batch 2i of its wave's 64, lane 32 + i batch 2i + 1.  After
+// the transform one v_permlane32_swap per pair of clerk rows leaves lane i holding batches
+// (2i, 2i+1) of row j and lane 32 + i the same batches of row j + 1: one 16-byte store per lane
+// per row pair (13 dwordx4 instead of 26 dwordx2 at n = 26) when WIDE (B even, 16-B aligned out).
+// (A persistent grid-stride variant was measured slower: the loop made hipcc keep the twiddle
+// words in SGPRs across tiles and spill.)
+template <int L, int N3, bool WIDE>
+__global__ __launch_bounds__(gen_block<L>()) __attribute__((amdgpu_waves_per_eu(SDA_GEN_WAVES)))
+void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const int64_t* __restrict__ draws,
+                       int64_t* __restrict__ out, uint32_t k, uint32_t t, uint64_t B,
+                       const GenTables* __restrict__ Tp, unsigned int* __restrict__ log) {
+    constexpr int LB = ilog(L, 2);
+    constexpr int ND = ilog(N3, 3);
+    constexpr int BS = gen_block<L>();
+    constexpr int NR = N3 - 1;         // share rows (clerks); N3 = 3^ND so NR is even
+    using Z = Zero3<L, N3>;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, half = lane >> 5;
+    const uint32_t lb = (tid & ~63u) + 2 * (lane & 31) + half;       // this lane's batch in the tile
+    const uint32_t pb_off = (tid & ~63u) + 2 * (lane & 31);          // first batch of its store pair
+    const MontP M = Tp->M;
+    const uint32_t p = M.p;
+    const int64_t P = (int64_t)p;
+    // LDS word e (batch-major [batch][k] secrets, then [batch][t] draws) lives at lpos(e): one pad
+    // word per 16 keeps the even/odd lane->batch reads below 2-way bank conflicted (b64 optimum).
+    __shared__ int64_t lds[BS * (L - 1) + BS * (L - 1) / 16 + 1];
+    auto lpos = [](uint32_t e) { return e + (e >> 4); };
+
+    {
+        const GenTables& T = *Tp;
+        const uint32_t vec = blockIdx.y;
+        const uint64_t b0 = (uint64_t)blockIdx.x * BS;
+        const int64_t* sec = secrets + (uint64_t)vec * D;
+
+        // ---- stage the tile's inputs through LDS with coalesced loads ----
+        // lds[0, BS k): the secrets of batches b0.. (zero past D: batched.rs:37-43 pads the tail
+        // batch); lds[BS k, BS (k + t)): their randomness.  U loads in flight before the first wait.
+        {
+            constexpr int U = 8;
+            const uint64_t nb = B - b0 < (uint64_t)BS ? B - b0 : (uint64_t)BS;
+            const uint64_t s0 = b0 * k;
+            const uint32_t ns = (uint32_t)nb * k;
+            const uint32_t valid = D > s0 ? (uint32_t)(D - s0 < ns ? D - s0 : ns) : 0u;
+            const int64_t* ssrc = sec + s0;
+            for (uint32_t base = 0; base < ns; base += U * BS) {
+                int64_t v[U];
+                static_for<0, U>([&](auto u) {
+                    const uint32_t e = base + u * BS + tid;
+                    v[u] = ssrc[e < valid ? e : 0];
+                });
+                static_for<0, U>([&](auto u) {
+                    const uint32_t e = base + u * BS + tid;
+                    if (e < ns) lds[lpos(e)] = e < valid ? v[u] : 0;
+                });
+            }
+            const uint32_t nd = (uint32_t)nb * t;
+            const int64_t* dsrc = draws + ((uint64_t)vec * B + b0) * t;
+            const uint32_t dbase = (uint32_t)BS * k;
+            for (uint32_t base = 0; base < nd; base += U * BS) {
+                int64_t v[U];
+                static_for<0, U>([&](auto u) {
+                    const uint32_t e = base + u * BS + tid;
+                    v[u] = dsrc[e < nd ? e : 0];
+                });
+                static_for<0, U>([&](auto u) {
+                    const uint32_t e = base + u * BS + tid;
+                    if (e < nd) lds[lpos(dbase + e)] = v[u];
+                });
+            }
+        }
+        __syncthreads();
+
+        // values = [0, secrets, randomness]; lanes past B run on zeros and store nothing
+        const uint64_t b = b0 + lb;
+        const bool live = b < B;
+        int64_t raw[L];
+        raw[0] = 0;
+        {
+            const uint32_t es = lb * k - 1;                                    // + i,      i <= k
+            const uint32_t ed = (uint32_t)BS * k + lb * t - 1 - k;             // + i,      i >  k
+            static_for<1, L>([&](auto i) { raw[i] = live ? lds[lpos(((uint32_t)i <= k ? es : ed) + i)] : 0; });
+        }
+        bool in_range = true;
+        static_for<1, L>([&](auto i) { in_range = in_range && ((uint64_t)(raw[i] + (P - 1)) < (uint64_t)(2 * P - 1)); });
+        // A store pair (see the lane map above) takes the fast path only when both of its batches
+        // are in range; otherwise both lanes log their batch for the generic exact fix-up kernel
+        // (rare: raw i64 secrets) and the fast path below stores nothing for the pair.  (A call
+        // to the generic path from inside this loop would force the live FFT state to spill.)
+        const uint32_t ok = in_range ? 1u : 0u;
+        const auto okx = __builtin_amdgcn_permlane32_swap(ok, ok, false, false);
+        const bool pair_ok = in_range && (half ? okx[0] : okx[1]);
+        if (live && !pair_ok) {                  // -> packed_gen_fixup_kernel
+            const uint32_t slot = atomicAdd(log, 1u);
+            if (slot < kGenLogCap) reinterpret_cast<uint64_t*>(log + 16)[slot] = (uint64_t)vec * B + b;
+        }
+
+        // ---- fft2_inverse: radix-2 DIT over omega_secrets^-1 on bit-reversed registers ----
+        FE x[L];
+        static_for<0, L>([&](auto i) {
+            const int32_t s = (int32_t)raw[i];
+            x[rev_digits(i, 2, LB)] = FE{s, canon32(s, p)};
+        });
+        static_for<1, LB + 1>([&](auto s) {
+            constexpr int H = 1 << (s - 1), LEN = 2 * H;
+            static_for<0, L, LEN>([&](auto g) {
+                static_for<0, H>([&](auto i) {
+                    if constexpr (i == 0) {
+                        bfly2_unit(x[g], x[g + H], p);
+                    } else {
+                        const int32_t w = (int32_t)T.tw2[H - 1 + i];
+                        bfly2(x[g + i], x[g + i + H], w, -w, T.tw2_m[H - 1 + i], M);
+                    }
+                });
+            });
+        });
+        // x * len_inv % p   (len_inv > 0 => the exact product has the sign of x)
+        static_for<0, L>([&](auto i) {
+            const uint32_t c = red1(redc_lazy((uint64_t)T.linv_m * x[i].c, M), p);
+            x[i] = FE{trunc_rep(c, (uint32_t)x[i].s, p), c};
+        });
+
+        // ---- fft3: radix-3 DIT over omega_shares on digit-reversed, zero-extended registers ----
+        FE y[N3];
+        static_for<0, N3>([&](auto i) {
+            if constexpr (i < L) y[rev_digits(i, 3, ND)] = x[i < L ? (int)i : 0];
+            else y[rev_digits(i, 3, ND)] = FE{0, 0};
+        });
+        static_for<1, ND + 1>([&](auto s) {
+            constexpr int th = ipow(3, s - 1);
+            constexpr int LEN = 3 * th, OB = (LEN - 3) / 2;
+            constexpr bool last = (s == ND);
+            static_for<0, N3, LEN>([&](auto g) {
+                static_for<0, th>([&](auto i) {
+                    constexpr bool zc = Z::is_zero(s - 1, g + i + th), zd = Z::is_zero(s - 1, g + i + 2 * th);
+                    if constexpr (zc && zd) {
+                        // (b + x 0 + x^2 0) % p == b for b in (-p, p): all three outputs are b
+                        y[g + i + th] = y[g + i];
+                        y[g + i + 2 * th] = y[g + i];
+                    } else {
+                        const FE bb = y[g + i], cc = y[g + i + th], dd = y[g + i + 2 * th];
+                        FE r[3];
+                        static_for<0, 3>([&](auto q) {
+                            constexpr int j = i + q * th;
+                            if constexpr (last && g + j == 0) {
+                                r[q] = FE{0, 0};            // points[0] is dropped (shares = points[1..])
+                            } else if constexpr (j == 0) {
+                                // x = x^2 = 1: (b + c + d) % p
+                                if constexpr (zd) {
+                                    const uint32_t c = addm(bb.c, cc.c, p);
+                                    r[q] = FE{trunc_rep(c, (uint32_t)__builtin_elementwise_add_sat(bb.s, cc.s), p), c};
+                                } else {
+                                    const int64_t v = (int64_t)bb.s + cc.s + dd.s;
+                                    const uint32_t c = addm(addm(bb.c, cc.c, p), dd.c, p);
+                                    r[q] = FE{trunc_rep(c, hi32(v), p), c};
+                                }
+                            } else if constexpr (zd) {
+                                const int32_t xw = (int32_t)T.tw3[OB + j];
+                                const int64_t v = (int64_t)bb.s + (int64_t)xw * cc.s;
+                                const uint32_t c = addm(bb.c, red1(redc_lazy((uint64_t)T.tw3_m[OB + j] * cc.c, M), p), p);
+                                r[q] = FE{trunc_rep(c, hi32(v), p), c};
+                            } else {
+                                // twiddles < p < 2^31: signed 32x32 products are exact (v_mad_i64_i32)
+                                const int32_t xw = (int32_t)T.tw3[OB + j], x2 = (int32_t)T.sq3[OB + j];
+                                const int64_t v = (int64_t)bb.s + (int64_t)xw * cc.s + (int64_t)x2 * dd.s;
+                                // residue: REDC(x' C + x2' D) + B    (x' C + x2' D < 2 p^2 < p R)
+                                const uint64_t acc = (uint64_t)T.tw3_m[OB + j] * cc.c + (uint64_t)T.sq3_m[OB + j] * dd.c;
+                                const uint32_t c = addm(bb.c, red1(redc_lazy(acc, M), p), p);
+                                r[q] = FE{trunc_rep(c, hi32(v), p), c};
+                            }
+                        });
+                        y[g + i] = r[0]; y[g + i + th] = r[1]; y[g + i + 2 * th] = r[2];
+                    }
+                });
+            });
+        });
+
+        // ---- shares = points[1..=n], clerk-major (batched.rs:46-48) ----
+        const uint64_t pb = b0 + pb_off;
+        const bool st1 = pair_ok && pb + 1 < B;
+        int64_t* orow = out + ((uint64_t)vec * NR + half) * B + pb;
+        if constexpr (WIDE) {              // B even => pb + 1 < B whenever pb < B
+            static_for<0, NR / 2>([&](auto q) {
+                const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)y[1 + 2 * q].s, (uint32_t)y[2 + 2 * q].s,
+                                                                false, false);
+                const int32_t lo = (int32_t)r[0], hi = (int32_t)r[1];  // batches pb, pb + 1 of row 1+2q+half
+                if (st1) {
+                    typedef int32_t v4i __attribute__((ext_vector_type(4)));
+                    v4i* d4 = reinterpret_cast<v4i*>(orow + (uint64_t)(2 * q) * B);
+                    const v4i val = {lo, lo >> 31, hi, hi >> 31};
+                    __builtin_nontemporal_store(val, d4);       // streamed once: keep it out of L2/MALL
+                }
+            });
+        } else {                           // odd B: each lane stores its own batch
+            int64_t* own = out + (uint64_t)vec * NR * B + b;
+            static_for<1, N3>([&](auto j) { if (live && pair_ok) own[(uint64_t)(j - 1) * B] = (int64_t)y[j].s; });
+        }
+    }
+}
+
+}  // namespace
+
+template <int L, int N3>
+static hipError_t gen_launch(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
+                             const GenFixupLog& log, hipStream_t s) {
+    constexpr int BS = gen_block<L>();
+    const uint64_t tiles_x = (B + BS - 1) / BS;
+    if (tiles_x > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)tiles_x, (unsigned)a.n_vectors);
+    if (B % 2 == 0 && ((uintptr_t)a.out % 16) == 0)
+        hipLaunchKernelGGL((packed_gen_kernel<L, N3, true>), grid, dim3(BS), 0, s, a.secrets, a.dimension, a.draws,
+                           a.out, k, t, B, T, log.count);
+    else
+        hipLaunchKernelGGL((packed_gen_kernel<L, N3, false>), grid, dim3(BS), 0, s, a.secrets, a.dimension, a.draws,
+                           a.out, k, t, B, T, log.count);
+    return hipGetLastError();
+}
+
+template <int N3>
+hipError_t gen_dispatch_L(uint32_t L, const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B,
+                          const GenTables* T, const GenFixupLog& log, hipStream_t s) {
+    switch (L) {
+        case 2: return gen_launch<2, N3>(a, k, t, B, T, log, s);
+        case 4: if constexpr (N3 >= 4) return gen_launch<4, N3>(a, k, t, B, T, log, s); break;
+        case 8: if constexpr (N3 >= 8) return gen_launch<8, N3>(a, k, t, B, T, log, s); break;
+        case 16: if constexpr (N3 >= 16) return gen_launch<16, N3>(a, k, t, B, T, log, s); break;
+        case 32: if constexpr (N3 >= 32) return gen_launch<32, N3>(a, k, t, B, T, log, s); break;
+        case 64: if constexpr (N3 >= 64) return gen_launch<64, N3>(a, k, t, B, T, log, s); break;
+    }
+    return hipErrorInvalidValue;
+}
+template hipError_t gen_dispatch_L<SDA_GEN_PART>(uint32_t, const PackedGenArgs&, uint32_t, uint32_t, uint64_t,
+                                                 const GenTables*, const GenFixupLog&, hipStream_t);
+
+#else  // dispatcher, tables, generic fix-up
+
 namespace {
 
 // ---------------- generic exact share (inputs outside (-p, p)) ----------------
@@ -54,253 +348,33 @@ __device__ __noinline__ void packed_share_generic(const int64_t* __restrict__ se
     for (int j = 1; j < N3; ++j) o[(uint64_t)(j - 1) * B] = y[j];
 }
 
-// A field element on the fast path: tss' exact representative s in (-p, p) and its canonical
-// residue c in [0, p).  Carrying both saves re-canonicalising every operand at every stage.
-struct FE {
-    int32_t s;
-    uint32_t c;
-};
-
-// radix-2 butterfly (u ± w c) % p.  The signs come from the exact i64 dividends (one
-// v_mad_i64_i32 each), the residues from one lazy Montgomery product shared by both outputs.
-__device__ __forceinline__ void bfly2(FE& u, FE& c, int32_t w, int32_t nw, uint32_t w_m, const MontP& M) {
-    const int64_t v1 = (int64_t)u.s + (int64_t)w * c.s;
-    const int64_t v2 = (int64_t)u.s + (int64_t)nw * c.s;
-    const uint32_t tc = red1(redc_lazy((uint64_t)w_m * c.c, M), M.p);
-    const uint32_t c1 = addm(u.c, tc, M.p), c2 = subm(u.c, tc, M.p);
-    u = FE{trunc_rep(c1, hi32(v1), M.p), c1};
-    c = FE{trunc_rep(c2, hi32(v2), M.p), c2};
-}
-
-// twiddle omega^0 = 1: (u + c) % p, (u - c) % p.  A saturating add keeps the exact sum's sign.
-__device__ __forceinline__ void bfly2_unit(FE& u, FE& c, uint32_t p) {
-    const uint32_t c1 = addm(u.c, c.c, p), c2 = subm(u.c, c.c, p);
-    const int32_t s1 = __builtin_elementwise_add_sat(u.s, c.s), s2 = __builtin_elementwise_sub_sat(u.s, c.s);
-    u = FE{trunc_rep(c1, (uint32_t)s1, p), c1};
-    c = FE{trunc_rep(c2, (uint32_t)s2, p), c2};
-}
-
-// Compile-time map of the radix-3 registers that hold a known zero (the zero padding of
-// coefficients L..N3-1) after `stage` levels: a group whose c and d are zero just copies b.
-template <int L, int N3>
-struct Zero3 {
-    static constexpr int ND = ilog(N3, 3);
-    static constexpr bool is_zero(int stage, int pos) {
-        if (stage == 0) return rev_digits(pos, 3, ND) >= L;
-        const int th = ipow(3, stage - 1), len = 3 * th;
-        const int g = pos - pos % len, i = (pos % len) % th;
-        return is_zero(stage - 1, g + i) && is_zero(stage - 1, g + i + th) && is_zero(stage - 1, g + i + 2 * th);
+// Batches the fast kernel logged (inputs outside (-p, p)), recomputed with the generic exact path.
+// If the log overflowed, every batch of the launch is recomputed (correct, slow, and only
+// reachable with raw i64 secrets far outside the field).
+__global__ __launch_bounds__(256) void packed_gen_fixup_kernel(const int64_t* __restrict__ secrets, uint64_t D,
+                                                               const int64_t* __restrict__ draws,
+                                                               int64_t* __restrict__ out, uint32_t k, uint32_t t,
+                                                               uint64_t B, uint64_t n_vec, int L, int N3,
+                                                               const GenTables* __restrict__ T, GenFixupLog log) {
+    const uint32_t n = *log.count;
+    if (n == 0) return;
+    const bool all = n > log.cap;
+    const uint64_t total = all ? B * n_vec : (uint64_t)n;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t gb = all ? i : log.list[i];
+        const uint64_t vec = gb / B, b = gb - vec * B;
+        packed_share_generic(secrets + vec * D, D, draws + gb * t, b, k, L, N3, *T,
+                             out + vec * (uint64_t)(N3 - 1) * B + b, B);
     }
-};
-
-// Workgroup size: 256 batches, fewer for the wide transforms so the LDS stage stays <= 32 KiB.
-template <int L>
-constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
-
-#ifndef SDA_GEN_WAVES
-#define SDA_GEN_WAVES 4
-#endif
-
-template <int L, int N3>
-__global__ __launch_bounds__(gen_block<L>()) __attribute__((amdgpu_waves_per_eu(SDA_GEN_WAVES)))
-void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const int64_t* __restrict__ draws,
-                       int64_t* __restrict__ out, uint32_t k, uint32_t t, uint64_t B,
-                       const GenTables* __restrict__ Tp) {
-    const GenTables& T = *Tp;          // global memory: uniform => scalar loads, no per-lane copy
-    constexpr int LB = ilog(L, 2);
-    constexpr int ND = ilog(N3, 3);
-    constexpr int BS = gen_block<L>();
-    using Z = Zero3<L, N3>;
-    const uint32_t tid = threadIdx.x;
-    const uint64_t b0 = (uint64_t)blockIdx.x * BS;
-    const uint64_t b = b0 + tid;
-    const uint64_t vec = blockIdx.y;
-    const int64_t* sec = secrets + vec * D;
-    const int64_t* drw = draws + (vec * B + b) * t;
-    const MontP M = T.M;
-    const uint32_t p = M.p;
-    const int64_t P = (int64_t)p;
-
-    // ---- stage this workgroup's inputs through LDS with coalesced loads ----
-    // lds[0, BS k): the secrets of batches b0.. (zero past D: batched.rs:37-43 pads the tail
-    // batch); lds[BS k, BS (k + t)): their randomness.  Loads are issued U at a time before
-    // the first wait.
-    __shared__ int64_t lds[BS * (L - 1)];
-    {
-        constexpr int U = 8;
-        const uint64_t nb = B - b0 < (uint64_t)BS ? B - b0 : (uint64_t)BS;
-        const uint64_t s0 = b0 * k;
-        const uint32_t ns = (uint32_t)nb * k;
-        const uint32_t valid = D > s0 ? (uint32_t)(D - s0 < ns ? D - s0 : ns) : 0u;
-        const int64_t* ssrc = sec + s0;
-        for (uint32_t base = 0; base < ns; base += U * BS) {
-            int64_t v[U];
-            static_for<0, U>([&](auto u) {
-                const uint32_t e = base + u * BS + tid;
-                v[u] = ssrc[e < valid ? e : 0];
-            });
-            static_for<0, U>([&](auto u) {
-                const uint32_t e = base + u * BS + tid;
-                if (e < ns) lds[e] = e < valid ? v[u] : 0;
-            });
-        }
-        const uint32_t nd = (uint32_t)nb * t;
-        const int64_t* dsrc = draws + (vec * B + b0) * t;
-        int64_t* ldr = lds + (uint32_t)BS * k;
-        for (uint32_t base = 0; base < nd; base += U * BS) {
-            int64_t v[U];
-            static_for<0, U>([&](auto u) {
-                const uint32_t e = base + u * BS + tid;
-                v[u] = dsrc[e < nd ? e : 0];
-            });
-            static_for<0, U>([&](auto u) {
-                const uint32_t e = base + u * BS + tid;
-                if (e < nd) ldr[e] = v[u];
-            });
-        }
-    }
-    __syncthreads();
-    if (b >= B) return;
-
-    // values = [0, secrets, randomness]
-    int64_t raw[L];
-    raw[0] = 0;
-    {
-        const int64_t* ls = lds + tid * k - 1;                              // + i,      i <= k
-        const int64_t* ld = lds + (uint32_t)BS * k + tid * t - 1 - k;       // + i,      i >  k
-#if SDA_GEN_EXPERIMENT == 1
-        static_for<1, L>([&](auto i) { raw[i] = (int64_t)((b * 2654435761u + i * 40503u) % p); });
-        (void)ls; (void)ld;
-#else
-        static_for<1, L>([&](auto i) { raw[i] = ((uint32_t)i <= k ? ls : ld)[i]; });
-#endif
-    }
-    bool in_range = true;
-    static_for<1, L>([&](auto i) { in_range = in_range && ((uint64_t)(raw[i] + (P - 1)) < (uint64_t)(2 * P - 1)); });
-
-    int64_t* o = out + vec * (uint64_t)(N3 - 1) * B + b;
-    if (!in_range) {
-        packed_share_generic(sec, D, drw, b, k, L, N3, T, o, B);
-        return;
-    }
-
-    // ---- fft2_inverse: radix-2 DIT over omega_secrets^-1 on bit-reversed registers ----
-    FE x[L];
-    static_for<0, L>([&](auto i) {
-        const int32_t s = (int32_t)raw[i];
-        x[rev_digits(i, 2, LB)] = FE{s, canon32(s, p)};
-    });
-    static_for<1, LB + 1>([&](auto s) {
-        constexpr int H = 1 << (s - 1), LEN = 2 * H;
-        static_for<0, L, LEN>([&](auto g) {
-            static_for<0, H>([&](auto i) {
-                if constexpr (i == 0) {
-                    bfly2_unit(x[g], x[g + H], p);
-                } else {
-                    const int32_t w = (int32_t)T.tw2[H - 1 + i];
-                    bfly2(x[g + i], x[g + i + H], w, -w, T.tw2_m[H - 1 + i], M);
-                }
-            });
-        });
-    });
-    // x * len_inv % p   (len_inv > 0 => the exact product has the sign of x)
-    static_for<0, L>([&](auto i) {
-        const uint32_t c = red1(redc_lazy((uint64_t)T.linv_m * x[i].c, M), p);
-        x[i] = FE{trunc_rep(c, (uint32_t)x[i].s, p), c};
-    });
-
-    // ---- fft3: radix-3 DIT over omega_shares on digit-reversed, zero-extended registers ----
-    FE y[N3];
-    static_for<0, N3>([&](auto i) {
-        if constexpr (i < L) y[rev_digits(i, 3, ND)] = x[i < L ? (int)i : 0];
-        else y[rev_digits(i, 3, ND)] = FE{0, 0};
-    });
-    static_for<1, ND + 1>([&](auto s) {
-        constexpr int th = ipow(3, s - 1);
-        constexpr int LEN = 3 * th, OB = (LEN - 3) / 2;
-        constexpr bool last = (s == ND);
-        static_for<0, N3, LEN>([&](auto g) {
-            static_for<0, th>([&](auto i) {
-                constexpr bool zc = Z::is_zero(s - 1, g + i + th), zd = Z::is_zero(s - 1, g + i + 2 * th);
-                if constexpr (zc && zd) {
-                    // (b + x 0 + x^2 0) % p == b for b in (-p, p): all three outputs are b
-                    y[g + i + th] = y[g + i];
-                    y[g + i + 2 * th] = y[g + i];
-                } else {
-                    const FE bb = y[g + i], cc = y[g + i + th], dd = y[g + i + 2 * th];
-                    FE r[3];
-                    static_for<0, 3>([&](auto q) {
-                        constexpr int j = i + q * th;
-                        if constexpr (last && g + j == 0) {
-                            r[q] = FE{0, 0};            // points[0] is dropped (shares = points[1..])
-                        } else if constexpr (j == 0) {
-                            // x = x^2 = 1: (b + c + d) % p
-                            if constexpr (zd) {
-                                const uint32_t c = addm(bb.c, cc.c, p);
-                                r[q] = FE{trunc_rep(c, (uint32_t)__builtin_elementwise_add_sat(bb.s, cc.s), p), c};
-                            } else {
-                                const int64_t v = (int64_t)bb.s + cc.s + dd.s;
-                                const uint32_t c = addm(addm(bb.c, cc.c, p), dd.c, p);
-                                r[q] = FE{trunc_rep(c, hi32(v), p), c};
-                            }
-                        } else if constexpr (zd) {
-                            const int32_t xw = (int32_t)T.tw3[OB + j];
-                            const int64_t v = (int64_t)bb.s + (int64_t)xw * cc.s;
-                            const uint32_t c = addm(bb.c, red1(redc_lazy((uint64_t)T.tw3_m[OB + j] * cc.c, M), p), p);
-                            r[q] = FE{trunc_rep(c, hi32(v), p), c};
-                        } else {
-                            // twiddles < p < 2^31: signed 32x32 products are exact (v_mad_i64_i32)
-                            const int32_t xw = (int32_t)T.tw3[OB + j], x2 = (int32_t)T.sq3[OB + j];
-                            const int64_t v = (int64_t)bb.s + (int64_t)xw * cc.s + (int64_t)x2 * dd.s;
-                            // residue: REDC(x' C + x2' D) + B    (x' C + x2' D < 2 p^2 < p R)
-                            const uint64_t acc = (uint64_t)T.tw3_m[OB + j] * cc.c + (uint64_t)T.sq3_m[OB + j] * dd.c;
-                            const uint32_t c = addm(bb.c, red1(redc_lazy(acc, M), p), p);
-                            r[q] = FE{trunc_rep(c, hi32(v), p), c};
-                        }
-                    });
-                    y[g + i] = r[0]; y[g + i + th] = r[1]; y[g + i + 2 * th] = r[2];
-                }
-            });
-        });
-    });
-    // shares = points[1..=n], clerk-major (batched.rs:46-48)
-#if SDA_GEN_EXPERIMENT == 2
-    int32_t acc = 0;
-    static_for<1, N3>([&](auto j) { acc ^= y[j].s; });
-    if (acc == 0x7fffffff) o[0] = acc;
-#else
-    static_for<1, N3>([&](auto j) { o[(uint64_t)(j - 1) * B] = (int64_t)y[j].s; });
-#endif
 }
 
 }  // namespace
 
-template <int L, int N3>
-static hipError_t gen_launch(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
-                             hipStream_t s) {
-    constexpr int BS = gen_block<L>();
-    dim3 grid((unsigned)((B + BS - 1) / BS), (unsigned)a.n_vectors);
-    hipLaunchKernelGGL((packed_gen_kernel<L, N3>), grid, dim3(BS), 0, s, a.secrets, a.dimension, a.draws, a.out,
-                       k, t, B, T);
-    return hipGetLastError();
-}
-
-template <int N3>
-static hipError_t gen_dispatch_L(uint32_t L, const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B,
-                                 const GenTables* T, hipStream_t s) {
-    switch (L) {
-        case 2: return gen_launch<2, N3>(a, k, t, B, T, s);
-        case 4: if constexpr (N3 >= 4) return gen_launch<4, N3>(a, k, t, B, T, s); break;
-        case 8: if constexpr (N3 >= 8) return gen_launch<8, N3>(a, k, t, B, T, s); break;
-        case 16: if constexpr (N3 >= 16) return gen_launch<16, N3>(a, k, t, B, T, s); break;
-        case 32: if constexpr (N3 >= 32) return gen_launch<32, N3>(a, k, t, B, T, s); break;
-        case 64: if constexpr (N3 >= 64) return gen_launch<64, N3>(a, k, t, B, T, s); break;
-    }
-    return hipErrorInvalidValue;
-}
+size_t packed_gen_log_bytes() { return 64 + (size_t)kGenLogCap * sizeof(uint64_t); }
 
 hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t, uint32_t n, uint32_t p,
-                                  uint32_t omega_secrets, uint32_t omega_shares, DeviceTable& tab, hipStream_t s) {
+                                  uint32_t omega_secrets, uint32_t omega_shares, DeviceTable& tab, void* log_buf,
+                                  hipStream_t s) {
     const uint32_t L = k + t + 1, N3 = n + 1;
     const uint64_t B = (a.dimension + k - 1) / k;
     if (B == 0 || a.n_vectors == 0) return hipSuccess;
@@ -312,17 +386,21 @@ hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t
         if (e != hipSuccess) return e;
     }
     const GenTables* T = static_cast<const GenTables*>(tab.dev);
-#ifdef SDA_ISA_ONLY      // developer switch: one instantiation, for ISA inspection
-    if (L == 16 && N3 == 27) return gen_launch<16, 27>(a, k, t, B, T, s);
-#else
+    GenFixupLog log{static_cast<unsigned int*>(log_buf),
+                    reinterpret_cast<uint64_t*>(static_cast<unsigned int*>(log_buf) + 16), kGenLogCap};
+    hipError_t e = hipMemsetAsync(log.count, 0, sizeof(unsigned int), s);
+    if (e != hipSuccess) return e;
     switch (N3) {
-        case 3: return gen_dispatch_L<3>(L, a, k, t, B, T, s);
-        case 9: return gen_dispatch_L<9>(L, a, k, t, B, T, s);
-        case 27: return gen_dispatch_L<27>(L, a, k, t, B, T, s);
-        case 81: return gen_dispatch_L<81>(L, a, k, t, B, T, s);
+        case 3: e = gen_dispatch_L<3>(L, a, k, t, B, T, log, s); break;
+        case 9: e = gen_dispatch_L<9>(L, a, k, t, B, T, log, s); break;
+        case 27: e = gen_dispatch_L<27>(L, a, k, t, B, T, log, s); break;
+        case 81: e = gen_dispatch_L<81>(L, a, k, t, B, T, log, s); break;
+        default: e = hipErrorInvalidValue;
     }
-#endif
-    return hipErrorInvalidValue;
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(packed_gen_fixup_kernel, dim3(256), dim3(256), 0, s, a.secrets, a.dimension, a.draws, a.out,
+                       k, t, B, a.n_vectors, (int)L, (int)N3, T, log);
+    return hipGetLastError();
 }
 
 hipError_t ensure_table(DeviceTable& t, const std::vector<uint8_t>& key, const void* host, size_t bytes) {
@@ -348,5 +426,7 @@ void free_table(DeviceTable& t) {
     t.cap = 0;
     t.key.clear();
 }
+
+#endif  // SDA_GEN_PART
 
 }  // namespace sda

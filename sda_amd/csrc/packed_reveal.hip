@@ -4,11 +4,6 @@
 namespace sda {
 using namespace packed;
 
-namespace {
-
-// ------------------------------------------------------------------------------------------
-// reveal
-// ------------------------------------------------------------------------------------------
 // Device table (u32 words), stride TS = 128 (max points):
 //   [0, TS*TS)            inv[j][i]    canonical mod_inverse(points[i] - points[i-j])
 //   [TS*TS, 2 TS*TS)      inv_m[j][i]  Montgomery form
@@ -20,6 +15,15 @@ constexpr int KMAX = 64;
 constexpr size_t OFF_INV = 0, OFF_INVM = (size_t)TS * TS, OFF_NP = 2 * (size_t)TS * TS,
                  OFF_NPM = OFF_NP + (size_t)KMAX * TS, OFF_LAM = OFF_NPM + (size_t)KMAX * TS,
                  TAB_WORDS = OFF_LAM + (size_t)KMAX * TS;
+
+// One launcher per MM (the padded point count); each is compiled in its own object
+// (Makefile: -DSDA_REVEAL_PART=MM) so the wide instantiations build in parallel.
+template <int MM>
+hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32_t n_idx, uint32_t k,
+                         const uint32_t* tab, const MontP& M, hipStream_t s);
+
+#ifdef SDA_REVEAL_PART
+namespace {
 
 // A field element: tss' exact representative s in (-p, p) and its canonical residue c.
 struct FE {
@@ -66,7 +70,9 @@ __device__ __forceinline__ void reveal_flush(int64_t* lds_o, int64_t* o, uint64_
     }
 }
 
-template <int MMAX, bool STAGED>
+// KU > 0: the evaluation loop over the k <= KU secrets is unrolled (table offsets become
+// compile-time constants: merged scalar loads, no per-secret loop overhead).
+template <int MMAX, bool STAGED, int KU>
 __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t* __restrict__ shares, uint64_t B,
                                                                   uint64_t D, int64_t* __restrict__ out,
                                                                   uint32_t n_idx, uint32_t k,
@@ -104,21 +110,33 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
         // numtheory::compute_newton_coefficients: for j in 1..m { for i in (j..m).rev() {
         //   s[i] = (((s[i] - s[i-1]) % p) * inv(points[i] - points[i-j])) % p } }
         // inv >= 0, so the product has the sign of the exact difference (or is 0).
-        static_for<1, MMAX>([&](auto j) {
-            if ((uint32_t)j < m) {
-                static_for<0, MMAX - j>([&](auto ii) {
+        auto newton_step = [&](auto i, uint32_t j) {
+            const uint32_t dc = s[i].c - s[i - 1].c + p;      // lazy: (0, 2p), REDC input < 2p^2 < pR
+            const int32_t sg = __builtin_elementwise_sub_sat(s[i].s, s[i - 1].s);
+            const uint32_t fc = red1(redc_lazy((uint64_t)tab[OFF_INVM + j * TS + i] * dc, M), p);
+            s[i] = FE{trunc_rep(fc, (uint32_t)sg, p), fc};
+        };
+        if constexpr (MMAX <= 16) {
+            // fully unrolled triangle: every table word is a compile-time offset (merged s_loads)
+            static_for<1, MMAX>([&](auto j) {
+                if ((uint32_t)j < m) {
+                    static_for<0, MMAX - j>([&](auto ii) {
+                        constexpr int i = MMAX - 1 - ii;
+                        if ((uint32_t)i < m) newton_step(std::integral_constant<int, i>{}, (uint32_t)j);
+                    });
+                }
+            });
+        } else {
+            // wide index sets: runtime j, unrolled i (uniform branches); keeps code size O(MMAX)
+            for (uint32_t j = 1; j < m; ++j) {
+                static_for<0, MMAX - 1>([&](auto ii) {
                     constexpr int i = MMAX - 1 - ii;
-                    if ((uint32_t)i < m) {
-                        const uint32_t dc = subm(s[i].c, s[i - 1].c, p);
-                        const int32_t sg = __builtin_elementwise_sub_sat(s[i].s, s[i - 1].s);
-                        const uint32_t fc = red1(redc_lazy((uint64_t)tab[OFF_INVM + j * TS + i] * dc, M), p);
-                        s[i] = FE{trunc_rep(fc, (uint32_t)sg, p), fc};
-                    }
+                    if ((uint32_t)i < m && (uint32_t)i >= j) newton_step(std::integral_constant<int, i>{}, j);
                 });
             }
-        });
+        }
         // numtheory::newton_evaluate at omega_secrets^(e+1): fold((a + (coef * np) % p) % p)
-        for (uint32_t e = 0; e < k; ++e) {
+        auto eval = [&](uint32_t e) {
             const uint32_t* np = tab + OFF_NP + e * TS;
             const uint32_t* npm = tab + OFF_NPM + e * TS;
             FE acc{0, 0};
@@ -131,6 +149,11 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
                 }
             });
             if (e < lim) dst[e] = acc.s;                                                // batched.rs:94
+        };
+        if constexpr (KU > 0) {
+            static_for<0, KU>([&](auto e) { if ((uint32_t)e < k) eval((uint32_t)e); });
+        } else {
+            for (uint32_t e = 0; e < k; ++e) eval(e);
         }
     }
     reveal_flush<STAGED>(lds_o, o, b0, B, D, k);
@@ -186,6 +209,36 @@ __global__ __launch_bounds__(256) void packed_reveal_canon_kernel(const int64_t*
 
 }  // namespace
 
+template <int MM>
+hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32_t n_idx, uint32_t k,
+                         const uint32_t* tab, const MontP& M, hipStream_t s) {
+    dim3 grid((unsigned)((B + 255) / 256), (unsigned)a.n_vectors);
+    const bool staged = k <= 16;                      // LDS stage: 256 * k * 8 B <= 32 KiB
+    const size_t lds = staged ? (size_t)256 * k * sizeof(int64_t) : 0;
+    if (mode == 0) {
+        if (staged && k <= 8 && MM <= 16)
+            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8>), grid, dim3(256), lds, s, a.shares, B,
+                               a.dimension, a.out, n_idx, k, tab, M);
+        else if (staged)
+            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 0>), grid, dim3(256), lds, s, a.shares, B,
+                               a.dimension, a.out, n_idx, k, tab, M);
+        else
+            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, false, 0>), grid, dim3(256), 0, s, a.shares, B,
+                               a.dimension, a.out, n_idx, k, tab, M);
+    } else {
+        if (staged)
+            hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, true>), grid, dim3(256), lds, s, a.shares, B,
+                               a.dimension, a.out, n_idx, k, tab, M);
+        else
+            hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, false>), grid, dim3(256), 0, s, a.shares, B,
+                               a.dimension, a.out, n_idx, k, tab, M);
+    }
+    return hipGetLastError();
+}
+template hipError_t reveal_launch<SDA_REVEAL_PART>(int, const PackedRevealArgs&, uint64_t, uint32_t, uint32_t,
+                                                   const uint32_t*, const MontP&, hipStream_t);
+
+#else  // dispatcher + host tables
 
 // Host precompute of the per-index-set tables (data independent; same ops as tss).
 static void build_reveal_tables(std::vector<uint32_t>& tab, const uint64_t* indices, uint32_t n_idx, uint32_t k,
@@ -231,30 +284,6 @@ static void build_reveal_tables(std::vector<uint32_t>& tab, const uint64_t* indi
     }
 }
 
-template <int MM>
-static hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32_t n_idx, uint32_t k,
-                                const uint32_t* tab, const MontP& M, hipStream_t s) {
-    dim3 grid((unsigned)((B + 255) / 256), (unsigned)a.n_vectors);
-    const bool staged = k <= 16;                      // LDS stage: 256 * k * 8 B <= 32 KiB
-    const size_t lds = staged ? (size_t)256 * k * sizeof(int64_t) : 0;
-    if (mode == 0) {
-        if (staged)
-            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true>), grid, dim3(256), lds, s, a.shares, B,
-                               a.dimension, a.out, n_idx, k, tab, M);
-        else
-            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, false>), grid, dim3(256), 0, s, a.shares, B,
-                               a.dimension, a.out, n_idx, k, tab, M);
-    } else {
-        if (staged)
-            hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, true>), grid, dim3(256), lds, s, a.shares, B,
-                               a.dimension, a.out, n_idx, k, tab, M);
-        else
-            hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, false>), grid, dim3(256), 0, s, a.shares, B,
-                               a.dimension, a.out, n_idx, k, tab, M);
-    }
-    return hipGetLastError();
-}
-
 hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indices, uint32_t n_idx, uint32_t k,
                                 uint32_t p, uint32_t omega_secrets, uint32_t omega_shares, int mode,
                                 DeviceTable& tab, hipStream_t s) {
@@ -276,14 +305,13 @@ hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indic
     const uint32_t* dtab = static_cast<const uint32_t*>(tab.dev);
     const uint32_t m = n_idx + 1;
     const uint32_t need = mode == 0 ? m : n_idx;
-#ifdef SDA_ISA_ONLY      // developer switch: one instantiation, for ISA inspection
-    if (need <= 16) return reveal_launch<16>(mode, a, B, n_idx, k, dtab, M, s);
-#endif
     if (need <= 8) return reveal_launch<8>(mode, a, B, n_idx, k, dtab, M, s);
     if (need <= 16) return reveal_launch<16>(mode, a, B, n_idx, k, dtab, M, s);
     if (need <= 32) return reveal_launch<32>(mode, a, B, n_idx, k, dtab, M, s);
     if (need <= 64) return reveal_launch<64>(mode, a, B, n_idx, k, dtab, M, s);
     return hipErrorInvalidValue;
 }
+
+#endif  // SDA_REVEAL_PART
 
 }  // namespace sda

@@ -129,3 +129,20 @@ def test_additive_generate_dev(engine, oracle):
     engine.additive_generate_dev(m, n, dsec.data_ptr(), D, ddr.data_ptr(), out.data_ptr(), _stream())
     torch.cuda.synchronize()
     assert (out.cpu().numpy() == oracle.additive_generate(m, n, sec, draws)).all()
+
+
+def test_packed_generate_fixup_overflow(engine, oracle):
+    """More out-of-range batches than the fix-up log holds: every batch is recomputed exactly."""
+    sch = S.CONFIG_PACKED
+    p, k, t, n = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count
+    B = 70_001                                  # > kGenLogCap (65536) logged batches, odd => narrow stores
+    D = B * k - 3
+    rng = np.random.default_rng(0x5DA)
+    sec = rng.integers(-(2**40), 2**40, size=D, dtype=np.int64)
+    draws = rng.integers(0, p - 1, size=(B, t), dtype=np.int64)
+    shares = engine.share_generate(sch, sec, draws.reshape(-1))
+    pp = oracle.packed_params(k, n, t, p, sch.omega_secrets, sch.omega_shares)
+    padded = np.concatenate([sec, np.zeros(B * k - D, dtype=np.int64)])
+    for b in list(np.random.default_rng(3).integers(0, B, 48)) + [0, B - 1]:
+        exp = oracle.packed_share(pp, padded[b * k:(b + 1) * k], draws[b])
+        assert_same(shares[:, b], exp)
