@@ -188,6 +188,41 @@ sda_status sda_chacha_mask_combine_dev(sda_engine* h, int64_t modulus, uint64_t 
                                        const uint32_t* seeds, uint64_t w, uint64_t n_seeds,
                                        int64_t* out, void* stream);
 
+/* ---------------- share payload codec ----------------
+ * Encryptor::encrypt encodes shares with integer-encoding 1.0 VarInt before sealing
+ * (client/src/crypto/encryption/sodium.rs:36-41); Decryptor::decrypt decodes after opening
+ * (:82-88): zigzag + LEB128, a run of >= 11 continuation bytes forms one 11-byte element and a
+ * truncated final varint yields its partial value.  The sealed box itself stays on the host. */
+
+/* Encryptor::encrypt's encoding step: out[*out_len] bytes (at most 10 per value). */
+sda_status sda_varint_encode(sda_engine* h, const int64_t* vals, uint64_t n,
+                             uint8_t* out, uint64_t out_cap, uint64_t* out_len);
+/* Decryptor::decrypt's decoding step for one opened blob. */
+sda_status sda_varint_decode(sda_engine* h, const uint8_t* bytes, uint64_t n_bytes,
+                             int64_t* out, uint64_t out_cap, uint64_t* out_len);
+/* Clerk job after the sealed-box opens (clerk.rs:79-86): decode every participation's blob,
+ * then ShareCombiner::combine -- "Wrong dimension" if a blob decodes to a different length. */
+sda_status sda_clerk_decode_combine(sda_engine* h, const sda_sharing_scheme* s,
+                                    const uint8_t* const* blobs, const uint64_t* blob_lens,
+                                    uint64_t n_blobs, int64_t* out, uint64_t out_cap,
+                                    uint64_t* out_len);
+/* Device forms.  `bytes`: device, 16-byte aligned, readable up to blob_off[n_blobs] rounded up to
+ * 16 plus 16 bytes; blob i = bytes[blob_off[i], blob_off[i+1]) with blob_off a HOST array.
+ * decode: out [n_blobs][out_stride] (device), counts[n_blobs] (host) = values per blob. */
+sda_status sda_varint_decode_dev(sda_engine* h, const uint8_t* bytes, const uint64_t* blob_off,
+                                 uint64_t n_blobs, int64_t* out, uint64_t out_stride,
+                                 uint64_t* counts, void* stream);
+/* decode + exact combine (combiner.rs:16-28); out (device) gets *out_len values. */
+sda_status sda_clerk_decode_combine_dev(sda_engine* h, int64_t modulus, const uint8_t* bytes,
+                                        const uint64_t* blob_off, uint64_t n_blobs,
+                                        int64_t* out, uint64_t out_cap, uint64_t* out_len,
+                                        void* stream);
+/* encode rows [rows][stride] (first len values of each) back to back into dst (device);
+ * row_bytes[rows] (host) = bytes per row. */
+sda_status sda_varint_encode_dev(sda_engine* h, const int64_t* vals, uint64_t rows, uint64_t len,
+                                 uint64_t stride, uint8_t* dst, uint64_t dst_cap,
+                                 uint64_t* row_bytes, void* stream);
+
 /* Synthetic benchmark input: dst[r*cols + c] = lo + splitmix64(seed, r, c) % (hi - lo). */
 sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64_t cols,
                               uint64_t seed, int64_t lo, int64_t hi, void* stream);

@@ -388,18 +388,26 @@ size_t or_varint_encode(const int64_t* vals, size_t n, uint8_t* out) {
     return w;
 }
 
+/* Decryptor::decrypt's loop (sodium.rs:82-88):
+ *     while reader.len() > 0 { let (i, size) = Share::decode_var(reader); push(i); reader = &reader[size..] }
+ * with integer-encoding 1.0 u64::decode_var (then zigzag for i64):
+ *     for b in src { result |= ((b & 0x7f) as u64) << shift; shift += 7;
+ *                    if b & 0x80 == 0 || shift > 10 * 7 { break } }      size = shift / 7
+ * Rust release builds mask an over-wide shift (`<< 70` == `<< 6`), reproduced with `& 63`, so a
+ * run of >= 11 continuation bytes becomes an 11-byte element, and a truncated final varint
+ * yields the partial value. */
 size_t or_varint_decode(const uint8_t* in, size_t n_bytes, int64_t* out, size_t cap) {
     size_t r = 0, c = 0;
     while (r < n_bytes && c < cap) {
         uint64_t z = 0;
-        int shift = 0;
-        for (;;) {
-            uint8_t b = in[r++];
-            z |= (uint64_t)(b & 0x7f) << shift;
+        unsigned shift = 0;
+        while (r < n_bytes) {
+            const uint8_t b = in[r++];
+            z |= (uint64_t)(b & 0x7f) << (shift & 63);
             shift += 7;
-            if (!(b & 0x80) || r >= n_bytes) break;
+            if (!(b & 0x80) || shift > 70) break;
         }
-        out[c++] = (int64_t)(z >> 1) ^ -(int64_t)(z & 1);
+        out[c++] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
     }
     return c;
 }

@@ -1,0 +1,450 @@
+// codec.hip -- share payload codec on gfx950.
+//
+// Reference: client/src/crypto/encryption/sodium.rs
+//   encrypt (:36-41):  for share in shares { size = share.encode_var(&mut buf); bytes.extend(&buf[..size]) }
+//   decrypt (:82-88):  while reader.len() > 0 { (i, size) = Share::decode_var(reader); push(i); reader = &reader[size..] }
+// with integer-encoding 1.0 VarInt for i64 (third-party, absent from the tree): zigzag
+// z = (v << 1) ^ (v >> 63), then LEB128 (7 bits per byte, low group first, 0x80 = "more").
+// u64::decode_var stops at the first byte without 0x80 or once shift > 70, so a run of >= 11
+// continuation bytes forms an 11-byte element whose 11th group lands at shift 70 & 63 (Rust
+// release semantics), and a truncated final varint yields its partial value.
+//
+// The clerk decrypts N participations (sodium stays on the host) and combines them
+// (clerk.rs:79-86).  On the device the blobs are one concatenated byte stream; decoding is a
+// stream compaction over terminator bytes (b & 0x80 == 0):
+//   pass A  per 4 KiB aligned region of a blob: count terminators, flag runs of >= 11
+//           continuation bytes ("irregular" blob);
+//   pass B  per blob: exclusive scan of its region counts -> element base per region, total;
+//   pass C  per region: each terminator byte decodes the <= 10-byte varint that ends at it (its
+//           start is the previous terminator, within the 16-byte halo) into out[blob][index].
+// Irregular blobs (malformed streams) are decoded by a sequential exact kernel instead.
+// Roofline: HBM.  Algorithmic bytes = payload bytes read + 8 B per decoded element written.
+#include "kernels.h"
+
+namespace sda {
+
+namespace {
+
+constexpr int kThreads = 256;                 // one 16-byte word per thread
+constexpr uint64_t kRegionBytes = kThreads * 16;
+
+// 16 bytes as a 16-bit mask of "continuation" bytes (bit j = byte j has 0x80).
+__device__ __forceinline__ uint32_t cont_mask(uint4 w) {
+    uint32_t m = 0;
+    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t hb = d[q] & 0x80808080u;
+        // gather bits 7, 15, 23, 31 into bits 0..3
+        const uint32_t g = (hb >> 7) | (hb >> 14) | (hb >> 21) | (hb >> 28);
+        m |= (g & 0xFu) << (4 * q);
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint8_t byte_of(const uint4& w, int j) {
+    const uint32_t d = j < 4 ? w.x : (j < 8 ? w.y : (j < 12 ? w.z : w.w));
+    return (uint8_t)(d >> (8 * (j & 3)));
+}
+
+// The region word this thread owns and its 32-byte window (previous word + own word):
+//   valid  bit j (16..31): window byte j is inside the blob
+//   term   bit j: a terminator (no 0x80) inside the blob, or the blob's last byte (truncated tail)
+//   cont   bit j: a continuation byte inside the blob (bytes outside the blob count as neither)
+struct Window {
+    uint4 prev, own;
+    uint32_t valid, term, cont;
+};
+
+__device__ __forceinline__ Window load_window(const uint8_t* __restrict__ base_aligned, uint64_t word, uint64_t begin,
+                                              uint64_t end) {
+    Window W;
+    const uint64_t a0 = word * 16;                      // byte offset of own word (aligned)
+    const uint4* p = reinterpret_cast<const uint4*>(base_aligned);
+    W.own = (a0 < end) ? p[word] : make_uint4(0, 0, 0, 0);
+    W.prev = (a0 >= 16 && a0 - 16 < end && a0 > begin) ? p[word - 1] : make_uint4(0, 0, 0, 0);
+    const uint32_t cm = cont_mask(W.prev) | (cont_mask(W.own) << 16);
+    // window byte j sits at a0 - 16 + j
+    uint32_t in = 0;
+    {
+        const int64_t lo = (int64_t)begin - (int64_t)(a0 - 16);   // first valid window index
+        const int64_t hi = (int64_t)end - (int64_t)(a0 - 16);     // one past last
+        const int l = lo < 0 ? 0 : (lo > 32 ? 32 : (int)lo);
+        const int h = hi < 0 ? 0 : (hi > 32 ? 32 : (int)hi);
+        if (h > l) in = (h - l == 32 ? 0xFFFFFFFFu : ((1u << (h - l)) - 1u)) << l;
+        W.valid = in & 0xFFFF0000u;
+        uint32_t lastbit = 0;
+        if (hi >= 1 && hi <= 32) lastbit = 1u << (hi - 1);      // the blob's last byte is in the window
+        W.cont = cm & in;
+        W.term = (~cm & in) | (lastbit & in);
+    }
+    return W;
+}
+
+// pass A: terminator count of each region; irregular-blob flag.
+__global__ __launch_bounds__(kThreads) void varint_count_kernel(const uint8_t* __restrict__ bytes,
+                                                                const uint64_t* __restrict__ region_word,
+                                                                const uint32_t* __restrict__ region_blob,
+                                                                const uint64_t* __restrict__ blob_off,
+                                                                uint32_t* __restrict__ region_count,
+                                                                uint32_t* __restrict__ blob_irregular) {
+    const uint32_t r = blockIdx.x;
+    const uint32_t b = region_blob[r];
+    const uint64_t word = region_word[r] + threadIdx.x;
+    const Window W = load_window(bytes, word, blob_off[b], blob_off[b + 1]);
+    uint32_t n = __builtin_popcount(W.term & W.valid);
+    // 11 continuation bytes in a row ending inside this word?
+    uint32_t run = W.cont;
+#pragma unroll
+    for (int k = 1; k <= 10; ++k) run &= W.cont << k;
+    if (run & W.valid) atomicOr(&blob_irregular[b], 1u);
+    // block reduction (one value per region)
+    __shared__ uint32_t red[kThreads / 64];
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+        for (int i = 0; i < kThreads / 64; ++i) s += red[i];
+        region_count[r] = s;
+    }
+}
+
+// pass B: per blob, exclusive scan of its region counts (regions of blob b are
+// [blob_region[b], blob_region[b+1])) -> region_base; total -> blob_count.
+__global__ __launch_bounds__(kThreads) void varint_scan_kernel(const uint32_t* __restrict__ region_count,
+                                                               const uint64_t* __restrict__ blob_region,
+                                                               uint64_t* __restrict__ region_base,
+                                                               uint64_t* __restrict__ blob_count) {
+    const uint32_t b = blockIdx.x;
+    const uint64_t r0 = blob_region[b], r1 = blob_region[b + 1];
+    __shared__ uint64_t part[kThreads];
+    uint64_t carry = 0;
+    for (uint64_t base = r0; base < r1; base += kThreads) {
+        const uint64_t r = base + threadIdx.x;
+        const uint64_t v = r < r1 ? region_count[r] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < kThreads; o <<= 1) {            // Hillis-Steele inclusive scan
+            const uint64_t add = threadIdx.x >= (uint32_t)o ? part[threadIdx.x - o] : 0;
+            __syncthreads();
+            part[threadIdx.x] += add;
+            __syncthreads();
+        }
+        if (r < r1) region_base[r] = carry + part[threadIdx.x] - v;
+        carry += part[kThreads - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) blob_count[b] = carry;
+}
+
+// pass C: decode.  Element index of a terminator = region base + terminators before it in the
+// region.  Rows: out + blob * out_stride; blobs flagged irregular (or whose count differs from
+// `len`) are skipped here.
+__global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* __restrict__ bytes,
+                                                                 const uint64_t* __restrict__ region_word,
+                                                                 const uint32_t* __restrict__ region_blob,
+                                                                 const uint64_t* __restrict__ blob_off,
+                                                                 const uint64_t* __restrict__ region_base,
+                                                                 const uint32_t* __restrict__ blob_irregular,
+                                                                 int64_t* __restrict__ out, uint64_t out_stride) {
+    const uint32_t r = blockIdx.x;
+    const uint32_t b = region_blob[r];
+    if (blob_irregular[b]) return;
+    const uint64_t word = region_word[r] + threadIdx.x;
+    const Window W = load_window(bytes, word, blob_off[b], blob_off[b + 1]);
+    const uint32_t tm = W.term & W.valid;
+    const uint32_t n = __builtin_popcount(tm);
+    // exclusive scan of n over the block
+    __shared__ uint32_t wsum[kThreads / 64];
+    uint32_t incl = n;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if ((threadIdx.x & 63) >= (uint32_t)o) incl += t;
+    }
+    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    uint32_t before = incl - n;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) before += wsum[w];
+    uint64_t idx = region_base[r] + before;
+    int64_t* row = out + (uint64_t)b * out_stride;
+    // terminators at window positions 16..31; the element starts after the previous terminator
+    // (or the blob start: bytes before it are neither term nor cont, i.e. a boundary)
+    const uint32_t boundary = W.term | ~(W.term | W.cont);    // a position that ends the previous element
+    uint32_t rem = tm;
+    while (rem) {
+        const int j = __builtin_ctz(rem);
+        rem &= rem - 1;
+        const uint32_t below = boundary & ((1u << j) - 1u);
+        const int s = below ? 32 - __builtin_clz(below) : 0;  // first byte of the element
+        uint64_t z = 0;
+        for (int q = s; q <= j; ++q) {
+            const uint8_t by = q < 16 ? byte_of(W.prev, q) : byte_of(W.own, q - 16);
+            z |= (uint64_t)(by & 0x7f) << (7 * (q - s));
+        }
+        row[idx++] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
+    }
+}
+
+// Irregular blobs: the reference loop, one lane per blob (only malformed streams get here).
+// With out == nullptr it only counts.
+__global__ void varint_sequential_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ blob_off,
+                                         uint32_t n_blobs, const uint32_t* __restrict__ blob_irregular,
+                                         uint64_t* __restrict__ blob_count, int64_t* __restrict__ out,
+                                         uint64_t out_stride, uint64_t cap) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n_blobs || !blob_irregular[b]) return;
+    uint64_t r = blob_off[b];
+    const uint64_t e = blob_off[b + 1];
+    uint64_t c = 0;
+    while (r < e) {
+        uint64_t z = 0;
+        unsigned shift = 0;
+        while (r < e) {
+            const uint8_t by = bytes[r++];
+            z |= (uint64_t)(by & 0x7f) << (shift & 63);
+            shift += 7;
+            if (!(by & 0x80) || shift > 70) break;
+        }
+        if (out && c < cap) out[(uint64_t)b * out_stride + c] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
+        ++c;
+    }
+    if (!out) blob_count[b] = c;
+}
+
+// ---------------- encode ----------------
+__device__ __forceinline__ uint32_t varint_size(int64_t v) {
+    const uint64_t z = ((uint64_t)v << 1) ^ (uint64_t)(v >> 63);
+    const int bits = 64 - __builtin_clzll(z | 1);
+    return (uint32_t)((bits + 6) / 7);
+}
+
+constexpr uint32_t kEncChunk = 4096;          // elements per encode block
+
+// sizes of each [row][chunk] block of elements
+__global__ __launch_bounds__(kThreads) void varint_size_kernel(const int64_t* __restrict__ vals, uint64_t len,
+                                                               uint64_t stride, uint32_t chunks,
+                                                               uint64_t* __restrict__ chunk_bytes) {
+    const uint32_t c = blockIdx.x, row = blockIdx.y;
+    const uint64_t e0 = (uint64_t)c * kEncChunk;
+    uint64_t n = 0;
+    for (uint32_t i = threadIdx.x; i < kEncChunk; i += kThreads)
+        if (e0 + i < len) n += varint_size(vals[row * stride + e0 + i]);
+    __shared__ uint64_t red[kThreads / 64];
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t s = 0;
+        for (int i = 0; i < kThreads / 64; ++i) s += red[i];
+        chunk_bytes[(uint64_t)row * chunks + c] = s;
+    }
+}
+
+// write: the block assembles its chunk's bytes in LDS (<= 10 B per element), then stores them
+// at the chunk's byte offset (chunk_off = row offset + exclusive scan of chunk_bytes).
+__global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* __restrict__ vals, uint64_t len,
+                                                                uint64_t stride, uint32_t chunks,
+                                                                const uint64_t* __restrict__ chunk_off,
+                                                                uint8_t* __restrict__ dst) {
+    const uint32_t c = blockIdx.x, row = blockIdx.y;
+    const uint64_t e0 = (uint64_t)c * kEncChunk;
+    constexpr uint32_t PER = kEncChunk / kThreads;            // 16 consecutive elements per thread
+    __shared__ uint8_t buf[kEncChunk * 10];
+    __shared__ uint32_t tsum[kThreads];
+    int64_t v[PER];
+    uint32_t sz = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint64_t e = e0 + threadIdx.x * PER + q;
+        v[q] = e < len ? vals[row * stride + e] : 0;
+        sz += e < len ? varint_size(v[q]) : 0;
+    }
+    tsum[threadIdx.x] = sz;
+    __syncthreads();
+    for (int o = 1; o < kThreads; o <<= 1) {
+        const uint32_t add = threadIdx.x >= (uint32_t)o ? tsum[threadIdx.x - o] : 0;
+        __syncthreads();
+        tsum[threadIdx.x] += add;
+        __syncthreads();
+    }
+    uint32_t w = tsum[threadIdx.x] - sz;
+    const uint32_t total = tsum[kThreads - 1];
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint64_t e = e0 + threadIdx.x * PER + q;
+        if (e >= len) break;
+        uint64_t z = ((uint64_t)v[q] << 1) ^ (uint64_t)(v[q] >> 63);
+        while (z >= 0x80) { buf[w++] = (uint8_t)(z | 0x80); z >>= 7; }
+        buf[w++] = (uint8_t)z;
+    }
+    __syncthreads();
+    uint8_t* o = dst + chunk_off[(uint64_t)row * chunks + c];
+    for (uint32_t i = threadIdx.x; i < total; i += kThreads) o[i] = buf[i];
+}
+
+// exclusive scan of chunk_bytes per row (one block per row) + row base; row_bytes = total
+__global__ __launch_bounds__(kThreads) void varint_offsets_kernel(const uint64_t* __restrict__ chunk_bytes,
+                                                                  uint32_t chunks, const uint64_t* __restrict__ row_base,
+                                                                  uint64_t* __restrict__ chunk_off,
+                                                                  uint64_t* __restrict__ row_bytes) {
+    const uint32_t row = blockIdx.x;
+    __shared__ uint64_t part[kThreads];
+    uint64_t carry = row_base ? row_base[row] : 0, total = 0;
+    for (uint32_t base = 0; base < chunks; base += kThreads) {
+        const uint32_t c = base + threadIdx.x;
+        const uint64_t v = c < chunks ? chunk_bytes[(uint64_t)row * chunks + c] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < kThreads; o <<= 1) {
+            const uint64_t add = threadIdx.x >= (uint32_t)o ? part[threadIdx.x - o] : 0;
+            __syncthreads();
+            part[threadIdx.x] += add;
+            __syncthreads();
+        }
+        if (c < chunks) chunk_off[(uint64_t)row * chunks + c] = carry + part[threadIdx.x] - v;
+        carry += part[kThreads - 1];
+        total += part[kThreads - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && row_bytes) row_bytes[row] = total;
+}
+
+}  // namespace
+
+// ---------------- host-side planning ----------------
+void varint_plan(const uint64_t* blob_off, uint64_t n_blobs, VarintPlan* plan) {
+    plan->region_word.clear();
+    plan->region_blob.clear();
+    plan->blob_region.assign(n_blobs + 1, 0);
+    for (uint64_t b = 0; b < n_blobs; ++b) {
+        plan->blob_region[b] = plan->region_word.size();
+        const uint64_t s = blob_off[b], e = blob_off[b + 1];
+        if (e > s)
+            for (uint64_t a = s / kRegionBytes * kRegionBytes; a < e; a += kRegionBytes) {
+                plan->region_word.push_back(a / 16);
+                plan->region_blob.push_back((uint32_t)b);
+            }
+    }
+    plan->blob_region[n_blobs] = plan->region_word.size();
+}
+
+size_t varint_plan_device_bytes(const VarintPlan& p, uint64_t n_blobs) {
+    const size_t R = p.region_word.size();
+    return 64 * 8 + R * (8 + 4 + 4 + 8) + (n_blobs + 1) * (8 + 8) + n_blobs * (4 + 8);
+}
+
+// Layout of the device workspace for the decode passes.
+struct DecodeWork {
+    uint64_t* region_word; uint32_t* region_blob; uint32_t* region_count; uint64_t* region_base;
+    uint64_t* blob_off; uint64_t* blob_region; uint32_t* irregular; uint64_t* blob_count;
+};
+static DecodeWork carve(void* work, size_t R, uint64_t n_blobs) {
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    char* p = static_cast<char*>(work);
+    DecodeWork w;
+    w.region_word = (uint64_t*)p; p += up(R * 8);
+    w.region_base = (uint64_t*)p; p += up(R * 8);
+    w.region_blob = (uint32_t*)p; p += up(R * 4);
+    w.region_count = (uint32_t*)p; p += up(R * 4);
+    w.blob_off = (uint64_t*)p; p += up((n_blobs + 1) * 8);
+    w.blob_region = (uint64_t*)p; p += up((n_blobs + 1) * 8);
+    w.irregular = (uint32_t*)p; p += up(n_blobs * 4);
+    w.blob_count = (uint64_t*)p;
+    return w;
+}
+size_t varint_decode_work_bytes(size_t regions, uint64_t n_blobs) {
+    return 8 * 256 + regions * 24 + (n_blobs + 1) * 16 + n_blobs * 12 + 4096;
+}
+
+hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
+                               const VarintPlan& plan, void* work, uint64_t* counts_host, bool* irregular_any,
+                               hipStream_t s) {
+    const size_t R = plan.region_word.size();
+    DecodeWork w = carve(work, R, n_blobs);
+    hipError_t e;
+    if (R && (e = hipMemcpyAsync(w.region_word, plan.region_word.data(), R * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if (R && (e = hipMemcpyAsync(w.region_blob, plan.region_blob.data(), R * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(w.blob_off, blob_off_host, (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(w.blob_region, plan.blob_region.data(), (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.irregular, 0, n_blobs * 4, s)) != hipSuccess) return e;
+    if (R) {
+        hipLaunchKernelGGL(varint_count_kernel, dim3((unsigned)R), dim3(kThreads), 0, s, bytes, w.region_word,
+                           w.region_blob, w.blob_off, w.region_count, w.irregular);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(varint_scan_kernel, dim3((unsigned)n_blobs), dim3(kThreads), 0, s, w.region_count,
+                       w.blob_region, w.region_base, w.blob_count);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(varint_sequential_kernel, dim3((unsigned)((n_blobs + 63) / 64)), dim3(64), 0, s, bytes,
+                       w.blob_off, (uint32_t)n_blobs, w.irregular, w.blob_count, (int64_t*)nullptr, 0, 0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    std::vector<uint32_t> irr(n_blobs);
+    if ((e = hipMemcpyAsync(counts_host, w.blob_count, n_blobs * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(irr.data(), w.irregular, n_blobs * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    *irregular_any = false;
+    for (uint64_t b = 0; b < n_blobs; ++b) *irregular_any |= irr[b] != 0;
+    return hipSuccess;
+}
+
+hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
+                                int64_t* out, uint64_t out_stride, uint64_t len, bool irregular_any,
+                                hipStream_t s) {
+    const size_t R = plan.region_word.size();
+    DecodeWork w = carve(work, R, n_blobs);
+    hipError_t e;
+    if (R) {
+        hipLaunchKernelGGL(varint_decode_kernel, dim3((unsigned)R), dim3(kThreads), 0, s, bytes, w.region_word,
+                           w.region_blob, w.blob_off, w.region_base, w.irregular, out, out_stride);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (irregular_any) {
+        hipLaunchKernelGGL(varint_sequential_kernel, dim3((unsigned)((n_blobs + 63) / 64)), dim3(64), 0, s, bytes,
+                           w.blob_off, (uint32_t)n_blobs, w.irregular, w.blob_count, out, out_stride, len);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+size_t varint_encode_work_bytes(uint64_t rows, uint64_t len) {
+    const uint64_t chunks = (len + kEncChunk - 1) / kEncChunk;
+    return 2 * rows * (chunks ? chunks : 1) * 8 + 2 * rows * 8 + 1024;
+}
+
+hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len, uint64_t stride, uint8_t* dst,
+                                uint64_t dst_cap, void* work, uint64_t* row_bytes_host, hipStream_t s) {
+    const uint64_t chunks = (len + kEncChunk - 1) / kEncChunk;
+    if (rows == 0) return hipSuccess;
+    uint64_t* chunk_bytes = static_cast<uint64_t*>(work);
+    uint64_t* chunk_off = chunk_bytes + rows * (chunks ? chunks : 1);
+    uint64_t* row_base = chunk_off + rows * (chunks ? chunks : 1);
+    uint64_t* rbytes = row_base + rows;
+    hipError_t e;
+    if (chunks == 0) {
+        for (uint64_t r = 0; r < rows; ++r) row_bytes_host[r] = 0;
+        return hipSuccess;
+    }
+    hipLaunchKernelGGL(varint_size_kernel, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s, vals, len,
+                       stride, (uint32_t)chunks, chunk_bytes);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // per-row totals first (row_base = nullptr), then the host places rows back to back
+    hipLaunchKernelGGL(varint_offsets_kernel, dim3((unsigned)rows), dim3(kThreads), 0, s, chunk_bytes,
+                       (uint32_t)chunks, (const uint64_t*)nullptr, chunk_off, rbytes);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(row_bytes_host, rbytes, rows * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    std::vector<uint64_t> base(rows);
+    uint64_t acc = 0;
+    for (uint64_t r = 0; r < rows; ++r) { base[r] = acc; acc += row_bytes_host[r]; }
+    if (acc > dst_cap) return hipErrorInvalidValue;
+    if ((e = hipMemcpyAsync(row_base, base.data(), rows * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(varint_offsets_kernel, dim3((unsigned)rows), dim3(kThreads), 0, s, chunk_bytes,
+                       (uint32_t)chunks, (const uint64_t*)row_base, chunk_off, (uint64_t*)nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(varint_write_kernel, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s, vals, len,
+                       stride, (uint32_t)chunks, chunk_off, dst);
+    return hipGetLastError();
+}
+
+}  // namespace sda

@@ -27,6 +27,10 @@ struct sda_engine {
     sda::DeviceTable gen_tab;     // packed-Shamir twiddles (per scheme)
     void* gen_log = nullptr;      // packed-Shamir generic fix-up log (sda::packed_gen_log_bytes())
     size_t gen_log_bytes = 0;
+    void* codec_work = nullptr;   // varint codec plan / scan workspace
+    size_t codec_work_bytes = 0;
+    void* codec_mat = nullptr;    // decoded [N][len] matrix of the clerk decode+combine path
+    size_t codec_mat_bytes = 0;
     sda::DeviceTable rev_tab;     // packed-Shamir Newton/Lagrange tables (per scheme + clerk set)
 };
 
@@ -196,6 +200,8 @@ void sda_engine_destroy(sda_engine* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->work) (void)hipFree(h->work);
     if (h->gen_log) (void)hipFree(h->gen_log);
+    if (h->codec_work) (void)hipFree(h->codec_work);
+    if (h->codec_mat) (void)hipFree(h->codec_mat);
     if (h->stage) (void)hipFree(h->stage);
     sda::free_table(h->gen_tab);
     sda::free_table(h->rev_tab);
@@ -591,6 +597,183 @@ sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64
     if (hi <= lo) return fail(SDA_ERR_INVALID_ARGUMENT, "need hi > lo");
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(sda::launch_synth_fill(dst, rows, cols, seed, lo, hi, pick(h, stream)));
+    return ok();
+}
+
+}  // extern "C"
+
+// ---------------- share payload codec (sodium.rs:36-41 / :82-88) ----------------
+namespace {
+
+// Plan + count N device-resident blobs; counts[n] on the host.
+sda_status codec_count(sda_engine* h, const uint8_t* bytes, const uint64_t* blob_off, uint64_t n_blobs,
+                       sda::VarintPlan* plan, uint64_t* counts, bool* irregular, hipStream_t st) {
+    if (((uintptr_t)bytes & 15) != 0) return fail(SDA_ERR_INVALID_ARGUMENT, "byte buffer must be 16-byte aligned");
+    for (uint64_t b = 0; b < n_blobs; ++b)
+        if (blob_off[b + 1] < blob_off[b]) return fail(SDA_ERR_INVALID_ARGUMENT, "blob offsets must be non-decreasing");
+    sda::varint_plan(blob_off, n_blobs, plan);
+    if (sda_status e = ensure(&h->codec_work, &h->codec_work_bytes,
+                              sda::varint_decode_work_bytes(plan->region_word.size(), n_blobs)))
+        return e;
+    HIP_TRY(sda::launch_varint_count(bytes, blob_off, n_blobs, *plan, h->codec_work, counts, irregular, st));
+    return SDA_OK;
+}
+
+// decode + combiner.rs:16-28 over device-resident blobs; out (device) gets out_len = count of blob 0
+sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const uint64_t* blob_off, uint64_t n_blobs,
+                          int64_t* out, uint64_t out_cap, uint64_t* out_len, hipStream_t st) {
+    *out_len = 0;
+    if (n_blobs == 0) return ok();                                  // combiner.rs:17: empty input
+    sda::VarintPlan plan;
+    std::vector<uint64_t> counts(n_blobs);
+    bool irregular = false;
+    if (sda_status e = codec_count(h, bytes, blob_off, n_blobs, &plan, counts.data(), &irregular, st)) return e;
+    const uint64_t dim = counts[0];
+    for (uint64_t i = 1; i < n_blobs; ++i)
+        if (counts[i] != dim)
+            return fail(SDA_ERR_WRONG_DIMENSION, "Wrong dimension (participation %llu decodes to %llu shares, expected %llu)",
+                        (unsigned long long)i, (unsigned long long)counts[i], (unsigned long long)dim);
+    int64_t mm;
+    if (dim) {
+        if (sda_status e = modulus_abs(m, &mm)) return e;
+    }
+    if (out_cap < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
+    *out_len = dim;
+    if (dim == 0) return ok();
+    if (sda_status e = ensure(&h->codec_mat, &h->codec_mat_bytes, n_blobs * dim * 8)) return e;
+    int64_t* mat = static_cast<int64_t*>(h->codec_mat);
+    HIP_TRY(sda::launch_varint_decode(bytes, n_blobs, plan, h->codec_work, mat, dim, dim, irregular, st));
+    HIP_TRY(sda::launch_combine_exact(mat, n_blobs, dim, dim, out, mm, st));
+    return SDA_OK;
+}
+
+// concatenate host blobs into a 16-byte aligned, padded device buffer
+sda_status upload_blobs(sda_engine* h, const uint8_t* const* blobs, const uint64_t* lens, uint64_t n,
+                        DevArena* a, uint8_t** dev, std::vector<uint64_t>* off) {
+    off->assign(n + 1, 0);
+    for (uint64_t i = 0; i < n; ++i) {
+        if (lens[i] && !blobs[i]) return fail(SDA_ERR_INVALID_ARGUMENT, "blob %llu is NULL", (unsigned long long)i);
+        (*off)[i + 1] = (*off)[i] + lens[i];
+    }
+    const uint64_t total = (*off)[n];
+    std::vector<uint8_t> host(total + 32, 0);
+    for (uint64_t i = 0; i < n; ++i)
+        if (lens[i]) memcpy(host.data() + (*off)[i], blobs[i], lens[i]);
+    *dev = a->take<uint8_t>(total + 32);
+    HIP_TRY(hipMemcpyAsync(*dev, host.data(), total + 32, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));       // `host` goes out of scope
+    return SDA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+sda_status sda_varint_encode(sda_engine* h, const int64_t* vals, uint64_t n, uint8_t* out, uint64_t out_cap,
+                             uint64_t* out_len) {
+    if (!h || !out_len || (n && !vals)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    *out_len = 0;
+    if (n == 0) return ok();
+    HIP_TRY(hipSetDevice(h->device));
+    DevArena a;
+    if (sda_status st = stage(h, rup(n * 8) + rup(n * 10 + 16), &a)) return st;
+    int64_t* dv = a.take<int64_t>(n);
+    uint8_t* db = a.take<uint8_t>(n * 10 + 16);
+    HIP_TRY(hipMemcpyAsync(dv, vals, n * 8, hipMemcpyHostToDevice, h->stream));
+    if (sda_status st = ensure(&h->codec_work, &h->codec_work_bytes, sda::varint_encode_work_bytes(1, n))) return st;
+    uint64_t bytes = 0;
+    HIP_TRY(sda::launch_varint_encode(dv, 1, n, n, db, n * 10 + 16, h->codec_work, &bytes, h->stream));
+    if (bytes > out_cap) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small (%llu bytes needed)",
+                                     (unsigned long long)bytes);
+    HIP_TRY(hipMemcpyAsync(out, db, bytes, hipMemcpyDeviceToHost, h->stream));
+    *out_len = bytes;
+    return finish(h);
+}
+
+sda_status sda_varint_decode(sda_engine* h, const uint8_t* bytes, uint64_t n_bytes, int64_t* out, uint64_t out_cap,
+                             uint64_t* out_len) {
+    if (!h || !out_len || (n_bytes && !bytes)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    *out_len = 0;
+    HIP_TRY(hipSetDevice(h->device));
+    DevArena a;
+    if (sda_status st = stage(h, rup(n_bytes + 32) + rup(n_bytes * 8 + 8), &a)) return st;
+    uint8_t* db;
+    std::vector<uint64_t> off;
+    const uint8_t* const blobs[1] = {bytes};
+    if (sda_status st = upload_blobs(h, blobs, &n_bytes, 1, &a, &db, &off)) return st;
+    int64_t* dv = a.take<int64_t>(n_bytes + 1);
+    sda::VarintPlan plan;
+    uint64_t count = 0;
+    bool irregular = false;
+    if (sda_status st = codec_count(h, db, off.data(), 1, &plan, &count, &irregular, h->stream)) return st;
+    if (count > out_cap) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small (%llu values)",
+                                     (unsigned long long)count);
+    HIP_TRY(sda::launch_varint_decode(db, 1, plan, h->codec_work, dv, count, count, irregular, h->stream));
+    if (count) HIP_TRY(hipMemcpyAsync(out, dv, count * 8, hipMemcpyDeviceToHost, h->stream));
+    *out_len = count;
+    return finish(h);
+}
+
+sda_status sda_clerk_decode_combine(sda_engine* h, const sda_sharing_scheme* s, const uint8_t* const* blobs,
+                                    const uint64_t* blob_lens, uint64_t n_blobs, int64_t* out, uint64_t out_cap,
+                                    uint64_t* out_len) {
+    if (!h || !s || !out_len || (n_blobs && (!blobs || !blob_lens))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    *out_len = 0;
+    HIP_TRY(hipSetDevice(h->device));
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n_blobs; ++i) total += blob_lens[i];
+    DevArena a;
+    if (sda_status st = stage(h, rup(total + 32) + rup(total * 8 + 8), &a)) return st;
+    uint8_t* db;
+    std::vector<uint64_t> off;
+    if (sda_status st = upload_blobs(h, blobs, blob_lens, n_blobs, &a, &db, &off)) return st;
+    int64_t* dout = a.take<int64_t>(total + 1);
+    uint64_t len = 0;
+    if (sda_status st = decode_combine(h, s->modulus, db, off.data(), n_blobs, dout, (uint64_t)-1, &len, h->stream))
+        return st;
+    if (out_cap < len) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
+    if (len) HIP_TRY(hipMemcpyAsync(out, dout, len * 8, hipMemcpyDeviceToHost, h->stream));
+    *out_len = len;
+    return finish(h);
+}
+
+sda_status sda_varint_decode_dev(sda_engine* h, const uint8_t* bytes, const uint64_t* blob_off, uint64_t n_blobs,
+                                 int64_t* out, uint64_t out_stride, uint64_t* counts, void* stream) {
+    if (!h || !blob_off || !counts || (n_blobs && (!bytes || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = pick(h, stream);
+    sda::VarintPlan plan;
+    bool irregular = false;
+    if (sda_status e = codec_count(h, bytes, blob_off, n_blobs, &plan, counts, &irregular, st)) return e;
+    for (uint64_t i = 0; i < n_blobs; ++i)
+        if (counts[i] > out_stride)
+            return fail(SDA_ERR_INVALID_ARGUMENT, "blob %llu decodes to %llu values > out_stride",
+                        (unsigned long long)i, (unsigned long long)counts[i]);
+    HIP_TRY(sda::launch_varint_decode(bytes, n_blobs, plan, h->codec_work, out, out_stride, out_stride, irregular, st));
+    return ok();
+}
+
+sda_status sda_clerk_decode_combine_dev(sda_engine* h, int64_t modulus, const uint8_t* bytes, const uint64_t* blob_off,
+                                        uint64_t n_blobs, int64_t* out, uint64_t out_cap, uint64_t* out_len,
+                                        void* stream) {
+    if (!h || !blob_off || !out_len || (n_blobs && !bytes)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    HIP_TRY(hipSetDevice(h->device));
+    if (sda_status e = decode_combine(h, modulus, bytes, blob_off, n_blobs, out, out_cap, out_len, pick(h, stream)))
+        return e;
+    return ok();
+}
+
+sda_status sda_varint_encode_dev(sda_engine* h, const int64_t* vals, uint64_t rows, uint64_t len, uint64_t stride,
+                                 uint8_t* dst, uint64_t dst_cap, uint64_t* row_bytes, void* stream) {
+    if (!h || !row_bytes || (rows && len && (!vals || !dst))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (rows > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 rows per call");
+    if (stride < len) return fail(SDA_ERR_INVALID_ARGUMENT, "stride < len");
+    HIP_TRY(hipSetDevice(h->device));
+    if (sda_status e = ensure(&h->codec_work, &h->codec_work_bytes, sda::varint_encode_work_bytes(rows, len))) return e;
+    hipError_t e = sda::launch_varint_encode(vals, rows, len, stride, dst, dst_cap, h->codec_work, row_bytes,
+                                             pick(h, stream));
+    if (e == hipErrorInvalidValue) return fail(SDA_ERR_INVALID_ARGUMENT, "dst_cap too small");
+    HIP_TRY(e);
     return ok();
 }
 

@@ -64,6 +64,30 @@ hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indic
                                 uint32_t p, uint32_t omega_secrets, uint32_t omega_shares, int mode,
                                 DeviceTable& tab, hipStream_t s);
 
+// ---- codec.hip (share payload codec: sodium.rs:36-41 / :82-88, integer-encoding 1.0 VarInt) ----
+// Host-side plan of the decode: blobs are split into 4 KiB regions aligned to the (16-byte
+// aligned) byte buffer; a region shared by two blobs appears once per blob.
+struct VarintPlan {
+    std::vector<uint64_t> region_word;   // first 16-byte word of the region
+    std::vector<uint32_t> region_blob;   // blob it is decoded for
+    std::vector<uint64_t> blob_region;   // [n_blobs + 1] first region of each blob
+};
+void varint_plan(const uint64_t* blob_off, uint64_t n_blobs, VarintPlan* plan);
+size_t varint_decode_work_bytes(size_t regions, uint64_t n_blobs);
+// element count of every blob (synchronous: copies n_blobs counts to the host)
+hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
+                               const VarintPlan& plan, void* work, uint64_t* counts_host, bool* irregular_any,
+                               hipStream_t s);
+// decode every blob into out + blob * out_stride (after launch_varint_count on the same work)
+hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
+                                int64_t* out, uint64_t out_stride, uint64_t len, bool irregular_any,
+                                hipStream_t s);
+size_t varint_encode_work_bytes(uint64_t rows, uint64_t len);
+// encode rows [rows][stride] (first len elements) back to back into dst; row_bytes_host gets each
+// row's byte count (synchronous).  hipErrorInvalidValue if dst_cap is too small.
+hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len, uint64_t stride, uint8_t* dst,
+                                uint64_t dst_cap, void* work, uint64_t* row_bytes_host, hipStream_t s);
+
 // ---- chacha.hip ----
 // Combine of n_seeds ChaCha mask streams (chacha.rs:57-76).  `work` must hold
 // chacha_work_bytes(...) bytes of device memory.

@@ -12,7 +12,7 @@ using namespace packed;
 //   [.. , +KMAX*TS)       lam_m[e][i]  Montgomery Lagrange weight of clerk i      (CANONICAL)
 constexpr int TS = 128;
 constexpr int KMAX = 64;
-constexpr size_t OFF_INV = 0, OFF_INVM = (size_t)TS * TS, OFF_NP = 2 * (size_t)TS * TS,
+[[maybe_unused]] constexpr size_t OFF_INV = 0, OFF_INVM = (size_t)TS * TS, OFF_NP = 2 * (size_t)TS * TS,
                  OFF_NPM = OFF_NP + (size_t)KMAX * TS, OFF_LAM = OFF_NPM + (size_t)KMAX * TS,
                  TAB_WORDS = OFF_LAM + (size_t)KMAX * TS;
 

@@ -45,6 +45,7 @@ REVEAL_CANONICAL = 1
 _i64p = C.POINTER(C.c_int64)
 _u64p = C.POINTER(C.c_uint64)
 _u32p = C.POINTER(C.c_uint32)
+_u8p = C.POINTER(C.c_uint8)
 _vp = C.c_void_p
 _st = C.c_int
 
@@ -83,6 +84,13 @@ SIGNATURES = [
     ("sda_additive_generate_dev", _st, [_vp, C.c_int64, C.c_uint64, _vp, C.c_uint64, _vp, _vp, _vp]),
     ("sda_chacha_mask_combine_dev", _st, [_vp, C.c_int64, C.c_uint64, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
     ("sda_synth_fill_dev", _st, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int64, C.c_int64, _vp]),
+    ("sda_varint_encode", _st, [_vp, _i64p, C.c_uint64, _u8p, C.c_uint64, _u64p]),
+    ("sda_varint_decode", _st, [_vp, _u8p, C.c_uint64, _i64p, C.c_uint64, _u64p]),
+    ("sda_clerk_decode_combine", _st, [_vp, C.POINTER(S.SharingSchemeC), C.POINTER(_u8p), _u64p, C.c_uint64,
+                                       _i64p, C.c_uint64, _u64p]),
+    ("sda_varint_decode_dev", _st, [_vp, _vp, _u64p, C.c_uint64, _vp, C.c_uint64, _u64p, _vp]),
+    ("sda_clerk_decode_combine_dev", _st, [_vp, C.c_int64, _vp, _u64p, C.c_uint64, _vp, C.c_uint64, _u64p, _vp]),
+    ("sda_varint_encode_dev", _st, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp, C.c_uint64, _u64p, _vp]),
 ]
 
 _lib = None
@@ -225,6 +233,35 @@ class Engine:
         _check(self.lib.sda_recipient_positive(self.h, modulus, _ptr(v), v.size, _ptr(out)))
         return out[: v.size]
 
+    # ---------------- share payload codec (sodium.rs:36-41 / :82-88) ----------------
+    def varint_encode(self, values) -> bytes:
+        v = _arr(values)
+        out = (C.c_uint8 * max(10 * v.size, 1))()
+        olen = C.c_uint64(0)
+        _check(self.lib.sda_varint_encode(self.h, _ptr(v), v.size, out, len(out), C.byref(olen)))
+        return bytes(out[: olen.value])
+
+    def varint_decode(self, data: bytes) -> np.ndarray:
+        src = (C.c_uint8 * max(len(data), 1)).from_buffer_copy(data or b"\0")
+        out = np.zeros(max(len(data), 1), np.int64)
+        olen = C.c_uint64(0)
+        _check(self.lib.sda_varint_decode(self.h, src, len(data), _ptr(out), out.size, C.byref(olen)))
+        return out[: olen.value]
+
+    def clerk_decode_combine(self, scheme, blobs: Sequence[bytes]) -> np.ndarray:
+        """clerk.rs:79-86 after the sealed-box opens: decode each participation, combine."""
+        s = scheme.c()
+        bufs = [(C.c_uint8 * max(len(b), 1)).from_buffer_copy(b or b"\0") for b in blobs]
+        n = len(bufs)
+        ptrs = (_u8p * max(n, 1))(*[C.cast(b, _u8p) for b in bufs])
+        lens = (C.c_uint64 * max(n, 1))(*[len(b) for b in blobs])
+        cap = max([len(b) for b in blobs] + [1])
+        out = np.zeros(cap, np.int64)
+        olen = C.c_uint64(0)
+        _check(self.lib.sda_clerk_decode_combine(self.h, C.byref(s), ptrs, lens, n, _ptr(out), out.size,
+                                                 C.byref(olen)))
+        return out[: olen.value]
+
     def synchronize(self):
         _check(self.lib.sda_engine_synchronize(self.h))
 
@@ -257,3 +294,24 @@ class Engine:
 
     def synth_fill_dev(self, dst_ptr, rows, cols, seed, lo, hi, stream=None):
         _check(self.lib.sda_synth_fill_dev(self.h, dst_ptr, rows, cols, seed, lo, hi, stream))
+
+    def varint_decode_dev(self, bytes_ptr, blob_off, out_ptr, out_stride, stream=None) -> np.ndarray:
+        off = _arr(blob_off, np.uint64)
+        n = off.size - 1
+        counts = np.zeros(max(n, 1), np.uint64)
+        _check(self.lib.sda_varint_decode_dev(self.h, bytes_ptr, _ptr(off, _u64p), n, out_ptr, out_stride,
+                                              _ptr(counts, _u64p), stream))
+        return counts[:n]
+
+    def clerk_decode_combine_dev(self, modulus, bytes_ptr, blob_off, out_ptr, out_cap, stream=None) -> int:
+        off = _arr(blob_off, np.uint64)
+        olen = C.c_uint64(0)
+        _check(self.lib.sda_clerk_decode_combine_dev(self.h, modulus, bytes_ptr, _ptr(off, _u64p), off.size - 1,
+                                                     out_ptr, out_cap, C.byref(olen), stream))
+        return olen.value
+
+    def varint_encode_dev(self, vals_ptr, rows, length, stride, dst_ptr, dst_cap, stream=None) -> np.ndarray:
+        rb = np.zeros(max(rows, 1), np.uint64)
+        _check(self.lib.sda_varint_encode_dev(self.h, vals_ptr, rows, length, stride, dst_ptr, dst_cap,
+                                              _ptr(rb, _u64p), stream))
+        return rb[:rows]

@@ -1,0 +1,122 @@
+"""GPU parity of the share payload codec against the oracle.
+
+Reference: client/src/crypto/encryption/sodium.rs:36-41 (encode), :82-88 (decode) with
+integer-encoding 1.0 VarInt for i64 (zigzag + LEB128; third-party, restated in the oracle and
+pinned by the protobuf sint64 known answers in test_oracle_golden.py).  Bit-exact.
+"""
+import numpy as np
+import pytest
+
+from sda_amd import SdaError, schemes as S
+from tests.util import assert_same
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+I64_MIN, I64_MAX = -(2**63), 2**63 - 1
+EDGE = [0, -1, 1, 63, -64, 64, -65, 8191, -8192, 8192, 2**31 - 1, -(2**31), 2**62, -(2**62) - 1,
+        I64_MIN, I64_MAX, 433, -432, 2147482800, -2147482800]
+
+
+def _values(rng, n):
+    """a mix of byte lengths: small, field-sized (~31 bit) and full-range values"""
+    kind = rng.integers(0, 4, size=n)
+    v = np.where(kind == 0, rng.integers(-200, 200, size=n),
+                 np.where(kind == 1, rng.integers(-(2**31), 2**31, size=n),
+                          np.where(kind == 2, rng.integers(-(2**45), 2**45, size=n),
+                                   rng.integers(I64_MIN, I64_MAX, size=n, dtype=np.int64))))
+    return v.astype(np.int64)
+
+
+def test_encode_matches_oracle(engine, oracle):
+    rng = np.random.default_rng(1)
+    for vals in (np.array(EDGE, np.int64), _values(rng, 1), _values(rng, 4095), _values(rng, 4096),
+                 _values(rng, 70_001), np.zeros(0, np.int64)):
+        assert engine.varint_encode(vals) == oracle.varint_encode(vals)
+
+
+def test_decode_matches_oracle(engine, oracle):
+    rng = np.random.default_rng(2)
+    for vals in (np.array(EDGE, np.int64), _values(rng, 3), _values(rng, 10_000), _values(rng, 123_457)):
+        data = oracle.varint_encode(vals)
+        got = engine.varint_decode(data)
+        assert_same(got, vals)
+        assert_same(got, oracle.varint_decode(data))
+    assert engine.varint_decode(b"").size == 0
+
+
+@pytest.mark.parametrize("blob", [
+    bytes([0x80]),                                   # truncated final varint -> partial value
+    bytes([0x05, 0xFF, 0xFF]),                        # value, then a truncated tail
+    bytes([0xFF] * 10 + [0x01]),                      # 10 continuation + terminator = one 11-byte element
+    bytes([0xFF] * 11 + [0x01]),                      # 11 continuation bytes: an 11-byte element, then 0x01
+    bytes([0xFF] * 25 + [0x02, 0x03]),                # long run: sequential (irregular) path
+    bytes([0xFF] * 10),                               # 10-byte truncated tail
+    bytes([0x80] * 9 + [0x00]),                       # overlong zero
+])
+def test_decode_malformed_like_reference(engine, oracle, blob):
+    assert_same(engine.varint_decode(blob), oracle.varint_decode(blob))
+
+
+def _pack(blobs, pad_to=16):
+    """concatenate blobs at arbitrary (unaligned) offsets into one 16-byte aligned device buffer"""
+    off = [0]
+    for b in blobs:
+        off.append(off[-1] + len(b))
+    host = b"".join(blobs) + bytes(32)
+    t = torch.frombuffer(bytearray(host), dtype=torch.uint8).cuda()
+    assert t.data_ptr() % 16 == 0
+    return t, off
+
+
+def test_decode_dev_many_blobs(engine, oracle):
+    rng = np.random.default_rng(3)
+    rows = [_values(rng, int(n)) for n in (0, 1, 5, 700, 4096, 9000, 1, 33_333)]
+    blobs = [oracle.varint_encode(r) for r in rows]
+    blobs[3] = blobs[3] + bytes([0xFF] * 14 + [0x7F])        # an irregular blob among regular ones
+    rows[3] = oracle.varint_decode(blobs[3])
+    t, off = _pack(blobs)
+    stride = max(r.size for r in rows)
+    out = torch.full((len(rows), stride), 7, dtype=torch.int64, device="cuda")
+    counts = engine.varint_decode_dev(t.data_ptr(), off, out.data_ptr(), stride)
+    assert counts.tolist() == [r.size for r in rows]
+    o = out.cpu().numpy()
+    for i, r in enumerate(rows):
+        assert_same(o[i, :r.size], r, f"blob {i}")
+
+
+def test_clerk_decode_combine(engine, oracle):
+    """clerk.rs:79-86: decrypted payloads -> decode -> ShareCombiner::combine (signed, order-dependent)"""
+    rng = np.random.default_rng(4)
+    m = 2147482801
+    x = rng.integers(-(m - 1), m, size=(37, 5003), dtype=np.int64)
+    blobs = [oracle.varint_encode(r) for r in x]
+    got = engine.clerk_decode_combine(S.Additive(3, m), blobs)
+    assert_same(got, oracle.combine(m, x))
+    # a participation of a different length: Err("Wrong dimension") (combiner.rs:21)
+    bad = blobs[:5] + [oracle.varint_encode(x[5][:-1])] + blobs[6:]
+    with pytest.raises(SdaError) as ei:
+        engine.clerk_decode_combine(S.Additive(3, m), bad)
+    assert ei.value.status == 3
+    assert engine.clerk_decode_combine(S.Additive(3, m), []).size == 0
+
+
+def test_clerk_decode_combine_dev_and_encode_dev(engine, oracle):
+    """device round trip at a larger size: encode_dev -> decode+combine_dev == combine"""
+    m = 2147482801
+    N, D = 64, 100_003
+    x = torch.empty((N, D), dtype=torch.int64, device="cuda")
+    engine.synth_fill_dev(x.data_ptr(), N, D, 0x5DA + 7, -(m - 1), m)
+    cap = N * D * 10 + 32
+    buf = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    row_bytes = engine.varint_encode_dev(x.data_ptr(), N, D, D, buf.data_ptr(), cap)
+    off = np.concatenate([[0], np.cumsum(row_bytes)]).astype(np.uint64)
+    xh = x.cpu().numpy()
+    host = buf[: int(off[-1])].cpu().numpy().tobytes()
+    for i in (0, 17, N - 1):                                   # bytes equal the oracle's encoding
+        assert host[int(off[i]):int(off[i + 1])] == oracle.varint_encode(xh[i])
+    out = torch.empty(D, dtype=torch.int64, device="cuda")
+    n = engine.clerk_decode_combine_dev(m, buf.data_ptr(), off, out.data_ptr(), D)
+    torch.cuda.synchronize()
+    assert n == D
+    assert_same(out.cpu().numpy(), oracle.combine(m, xh))

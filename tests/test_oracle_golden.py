@@ -188,6 +188,25 @@ def test_masking_roundtrip(oracle):
         assert comb.tolist() == mask.tolist()
 
 
+def test_varint_known_answers(oracle):
+    """integer-encoding 1.0 VarInt for i64 = protobuf sint64: ZigZag table and LEB128 examples from
+    the Protocol Buffers encoding guide (0->0, -1->1, 1->2, -2->3, 2^31-1 -> 2^32-2,
+    -2^31 -> 2^32-1; 300 -> ac 02)."""
+    zz = {0: 0, -1: 1, 1: 2, -2: 3, 2**31 - 1: 2**32 - 2, -(2**31): 2**32 - 1}
+    for v, z in zz.items():
+        enc = oracle.varint_encode(np.array([v], np.int64))
+        dec, shift = 0, 0
+        for b in enc:
+            dec |= (b & 0x7F) << shift
+            shift += 7
+        assert dec == z and all(b & 0x80 for b in enc[:-1]) and not enc[-1] & 0x80
+    assert oracle.varint_encode(np.array([150], np.int64)) == bytes([0xAC, 0x02])   # zigzag(150) = 300
+    assert oracle.varint_encode(np.array([-2**63, 2**63 - 1], np.int64)) == bytes([0xFF] * 9 + [0x01] + [0xFE] + [0xFF] * 8 + [0x01])
+    # the decode loop of sodium.rs:82-88 over malformed input (u64::decode_var: shift > 70 stops)
+    assert oracle.varint_decode(bytes([0x80])).tolist() == [0]
+    assert oracle.varint_decode(bytes([0xFF] * 11 + [0x01])).tolist() == [-2**63, -1]
+
+
 def test_varint_codec(oracle):
     vals = np.array([0, -1, 1, 63, -64, 64, 2**62, -2**63, 2**63 - 1, 433, -432], np.int64)
     enc = oracle.varint_encode(vals)
