@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-check", action="store_true", help="A/B helper: skip the side-leg round-trip checks")
-    ap.add_argument("--only", choices=["combine", "shamir", "chacha"], default=None,
+    ap.add_argument("--codec-rows", type=int, default=1000, help="participations in the codec leg")
+    ap.add_argument("--only", choices=["combine", "shamir", "chacha", "codec"], default=None,
                     help="profile helper: run just one leg (no JSON contract)")
     return ap.parse_args()
 
@@ -225,6 +226,55 @@ def main():
                           "mask_elems_per_s": Ns * Dc / (c_ms * 1e-3),
                           "chacha_blocks_per_s": Ns * Dc / 8 / (c_ms * 1e-3)}
         log(f"[chacha] {json.dumps(side['chacha'])}")
+
+    if not args.no_side and args.only in (None, "codec"):
+        # clerk payload path (clerk.rs:79-86 after the sealed-box opens): varint payloads of
+        # signed field shares -> decode -> exact combine; plus the encode of the same matrix.
+        Nc, Dc = args.codec_rows, 1_000_000
+        x = torch.empty((Nc, Dc), dtype=torch.int64, device=dev)
+        eng.synth_fill_dev(x.data_ptr(), Nc, Dc, SEED_BASE + 6, -(m - 1), m, stream())
+        cap = Nc * Dc * 6 + 32                          # |v| < 2^31 -> zigzag < 2^32 -> <= 5 bytes
+        buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        et, dt_, ct = Timer(torch), Timer(torch), Timer(torch)
+        rb = None
+        for i in range(3):
+            f = lambda: eng.varint_encode_dev(x.data_ptr(), Nc, Dc, Dc, buf.data_ptr(), cap, stream())  # noqa
+            if i:
+                et.record(f)
+            else:
+                rb = f()
+        rb = eng.varint_encode_dev(x.data_ptr(), Nc, Dc, Dc, buf.data_ptr(), cap, stream())
+        off = np.concatenate([[0], np.cumsum(rb)]).astype(np.uint64)
+        payload = float(off[-1])
+        mat = torch.empty((Nc, Dc), dtype=torch.int64, device=dev)
+        cout = torch.empty(Dc, dtype=torch.int64, device=dev)
+        for i in range(4):
+            f = lambda: eng.varint_decode_dev(buf.data_ptr(), off, mat.data_ptr(), Dc, stream())  # noqa
+            dt_.record(f) if i else f()
+        for i in range(4):
+            f = lambda: eng.clerk_decode_combine_dev(m, buf.data_ptr(), off, cout.data_ptr(), Dc, stream())  # noqa
+            ct.record(f) if i else f()
+        torch.cuda.synchronize()
+        if not args.no_check:
+            if not torch.equal(mat, x):
+                raise SystemExit("codec round trip FAILED")
+            cols = torch.randint(0, Dc, (2048,), device=dev)
+            ref = x[:, cols].cpu().numpy()
+            from oracle import oracle as O
+            if not np.array_equal(cout[cols].cpu().numpy(), O.combine(m, ref)):
+                raise SystemExit("codec decode+combine FAILED")
+        e_ms, d_ms, c_ms = et.mean_ms(), dt_.mean_ms(), ct.mean_ms()
+        side["codec"] = {
+            "config": f"varint payloads of {Nc} participations x 1M-dim signed field shares "
+                      f"({payload / Nc / Dc:.2f} B/share)",
+            "payload_bytes": payload,
+            "decode_ms": d_ms, "decode_payload_GBps": payload / (d_ms * 1e-3) / 1e9,
+            "decode_hbm_GBps": (payload + 8.0 * Nc * Dc) / (d_ms * 1e-3) / 1e9,
+            "decode_combine_ms": c_ms, "decode_combine_shares_per_s": Nc * Dc / (c_ms * 1e-3),
+            "encode_ms": e_ms, "encode_hbm_GBps": (payload + 8.0 * Nc * Dc) / (e_ms * 1e-3) / 1e9,
+        }
+        log(f"[codec] {json.dumps(side['codec'])}")
+        del x, buf, mat
 
     if args.only is not None:
         return

@@ -27,6 +27,9 @@ namespace {
 
 constexpr int kThreads = 256;                 // one 16-byte word per thread
 constexpr uint64_t kRegionBytes = kThreads * 16;
+#ifndef SDA_DECODE_STAGE_OUT
+#define SDA_DECODE_STAGE_OUT 0
+#endif
 
 // 16 bytes as a 16-bit mask of "continuation" bytes (bit j = byte j has 0x80).
 __device__ __forceinline__ uint32_t cont_mask(uint4 w) {
@@ -81,16 +84,30 @@ __device__ __forceinline__ Window load_window(const uint8_t* __restrict__ base_a
     return W;
 }
 
+// 2-D grid: blockIdx.y = blob (+ y0), blockIdx.x = region within the blob (4 KiB aligned to the
+// byte buffer).  Blocks past a blob's last region exit at once (payload blobs have near-equal sizes).
+__device__ __forceinline__ bool region_of(const uint64_t* __restrict__ blob_region,
+                                          const uint64_t* __restrict__ blob_off, uint32_t y0, uint32_t* blob,
+                                          uint64_t* region, uint64_t* word) {
+    const uint32_t b = y0 + blockIdx.y;
+    const uint64_t r0 = blob_region[b], r1 = blob_region[b + 1];
+    if (r0 + blockIdx.x >= r1) return false;
+    *blob = b;
+    *region = r0 + blockIdx.x;
+    *word = (blob_off[b] / kRegionBytes + blockIdx.x) * (kRegionBytes / 16);
+    return true;
+}
+
 // pass A: terminator count of each region; irregular-blob flag.
 __global__ __launch_bounds__(kThreads) void varint_count_kernel(const uint8_t* __restrict__ bytes,
-                                                                const uint64_t* __restrict__ region_word,
-                                                                const uint32_t* __restrict__ region_blob,
-                                                                const uint64_t* __restrict__ blob_off,
+                                                                const uint64_t* __restrict__ blob_region,
+                                                                const uint64_t* __restrict__ blob_off, uint32_t y0,
                                                                 uint32_t* __restrict__ region_count,
                                                                 uint32_t* __restrict__ blob_irregular) {
-    const uint32_t r = blockIdx.x;
-    const uint32_t b = region_blob[r];
-    const uint64_t word = region_word[r] + threadIdx.x;
+    uint32_t b;
+    uint64_t r, word;
+    if (!region_of(blob_region, blob_off, y0, &b, &r, &word)) return;
+    word += threadIdx.x;
     const Window W = load_window(bytes, word, blob_off[b], blob_off[b + 1]);
     uint32_t n = __builtin_popcount(W.term & W.valid);
     // 11 continuation bytes in a row ending inside this word?
@@ -138,52 +155,90 @@ __global__ __launch_bounds__(kThreads) void varint_scan_kernel(const uint32_t* _
     if (threadIdx.x == 0) blob_count[b] = carry;
 }
 
-// pass C: decode.  Element index of a terminator = region base + terminators before it in the
-// region.  Rows: out + blob * out_stride; blobs flagged irregular (or whose count differs from
-// `len`) are skipped here.
+// 7-bit groups of the (zero-padded past the element) little-endian bytes of `x`, packed:
+// group i -> bits 7i..7i+6  (LEB128 payload of up to 8 bytes).
+__device__ __forceinline__ uint64_t leb_pack8(uint64_t x) {
+    x &= 0x7F7F7F7F7F7F7F7Full;
+    x = (x & 0x007F007F007F007Full) | ((x & 0x7F007F007F007F00ull) >> 1);
+    x = (x & 0x00003FFF00003FFFull) | ((x & 0x3FFF00003FFF0000ull) >> 2);
+    x = (x & 0x000000000FFFFFFFull) | ((x & 0x0FFFFFFF00000000ull) >> 4);
+    return x;
+}
+
+// pass C: decode.  The region's bytes (plus a 16-byte halo on each side) are staged in LDS; each
+// terminator byte decodes the varint ending at it from three funnel-shifted dwords; the values are
+// parked in LDS by element index and written back with coalesced stores.  Element index of a
+// terminator = region base + terminators before it in the region.  Blobs flagged irregular are
+// skipped here (varint_sequential_kernel).
 __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* __restrict__ bytes,
-                                                                 const uint64_t* __restrict__ region_word,
-                                                                 const uint32_t* __restrict__ region_blob,
-                                                                 const uint64_t* __restrict__ blob_off,
+                                                                 const uint64_t* __restrict__ blob_region,
+                                                                 const uint64_t* __restrict__ blob_off, uint32_t y0,
                                                                  const uint64_t* __restrict__ region_base,
                                                                  const uint32_t* __restrict__ blob_irregular,
                                                                  int64_t* __restrict__ out, uint64_t out_stride) {
-    const uint32_t r = blockIdx.x;
-    const uint32_t b = region_blob[r];
-    if (blob_irregular[b]) return;
-    const uint64_t word = region_word[r] + threadIdx.x;
+    uint32_t b;
+    uint64_t r, word;
+    if (!region_of(blob_region, blob_off, y0, &b, &r, &word) || blob_irregular[b]) return;
+    __shared__ uint32_t lb[(kRegionBytes + 32) / 4];          // [halo 16 B | region 4 KiB | tail 16 B]
+#if SDA_DECODE_STAGE_OUT
+    __shared__ int64_t lv[kRegionBytes];                      // decoded values by region-local index
+#endif
+    __shared__ uint32_t wsum[kThreads / 64];
+    word += threadIdx.x;
     const Window W = load_window(bytes, word, blob_off[b], blob_off[b + 1]);
+    reinterpret_cast<uint4*>(lb)[threadIdx.x + 1] = W.own;
+    if (threadIdx.x == 0) reinterpret_cast<uint4*>(lb)[0] = W.prev;
+    if (threadIdx.x == kThreads - 1) reinterpret_cast<uint4*>(lb)[kThreads + 1] = make_uint4(0, 0, 0, 0);
     const uint32_t tm = W.term & W.valid;
     const uint32_t n = __builtin_popcount(tm);
-    // exclusive scan of n over the block
-    __shared__ uint32_t wsum[kThreads / 64];
-    uint32_t incl = n;
+    uint32_t incl = n;                                        // exclusive scan of n over the block
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t t = __shfl_up(incl, o);
         if ((threadIdx.x & 63) >= (uint32_t)o) incl += t;
     }
     if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
     __syncthreads();
-    uint32_t before = incl - n;
-    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) before += wsum[w];
-    uint64_t idx = region_base[r] + before;
-    int64_t* row = out + (uint64_t)b * out_stride;
-    // terminators at window positions 16..31; the element starts after the previous terminator
-    // (or the blob start: bytes before it are neither term nor cont, i.e. a boundary)
-    const uint32_t boundary = W.term | ~(W.term | W.cont);    // a position that ends the previous element
+    uint32_t e = incl - n;
+    uint32_t total = 0;
+    for (uint32_t w = 0; w < kThreads / 64; ++w) {
+        if (w < (threadIdx.x >> 6)) e += wsum[w];
+        total += wsum[w];
+    }
+    // the element ending at window position j starts after the previous boundary (a terminator or
+    // a byte outside the blob)
+    const uint32_t boundary = W.term | ~(W.term | W.cont);
+    int64_t* dst = out + (uint64_t)b * out_stride + region_base[r];
+    (void)total;
     uint32_t rem = tm;
     while (rem) {
         const int j = __builtin_ctz(rem);
         rem &= rem - 1;
         const uint32_t below = boundary & ((1u << j) - 1u);
-        const int s = below ? 32 - __builtin_clz(below) : 0;  // first byte of the element
-        uint64_t z = 0;
-        for (int q = s; q <= j; ++q) {
-            const uint8_t by = q < 16 ? byte_of(W.prev, q) : byte_of(W.own, q - 16);
-            z |= (uint64_t)(by & 0x7f) << (7 * (q - s));
+        const int st = below ? 32 - __builtin_clz(below) : 0;      // window index of the first byte
+        const int len = j - st + 1;                                 // 1..11 on regular blobs
+        const uint32_t P = threadIdx.x * 16 + st;                   // byte position in lb
+        const uint32_t q = P >> 2, sh = (P & 3) * 8;
+        const uint32_t d0 = lb[q], d1 = lb[q + 1], d2 = lb[q + 2], d3 = lb[q + 3];
+        const uint32_t b0 = __builtin_amdgcn_alignbit(d1, d0, sh), b1 = __builtin_amdgcn_alignbit(d2, d1, sh),
+                       b2 = __builtin_amdgcn_alignbit(d3, d2, sh);
+        uint64_t lo = ((uint64_t)b1 << 32) | b0;
+        if (len < 8) lo &= (1ull << (8 * len)) - 1;
+        uint64_t z = leb_pack8(lo);
+        if (len > 8) {                  // groups 8, 9, 10 at shifts 56, 63, 70 & 63 = 6 (Rust release)
+            const uint32_t hb = b2 & ((len >= 11) ? 0xFFFFFFu : (len == 10 ? 0xFFFFu : 0xFFu));
+            z |= ((uint64_t)(hb & 0x7F) << 56) | ((uint64_t)((hb >> 8) & 0x7F) << 63) |
+                 ((uint64_t)((hb >> 16) & 0x7F) << 6);
         }
-        row[idx++] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
+#if SDA_DECODE_STAGE_OUT
+        lv[e++] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
+#else
+        dst[e++] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
+#endif
     }
+#if SDA_DECODE_STAGE_OUT
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < total; i += kThreads) dst[i] = lv[i];
+#endif
 }
 
 // Irregular blobs: the reference loop, one lane per blob (only malformed streams get here).
@@ -314,38 +369,30 @@ __global__ __launch_bounds__(kThreads) void varint_offsets_kernel(const uint64_t
 
 // ---------------- host-side planning ----------------
 void varint_plan(const uint64_t* blob_off, uint64_t n_blobs, VarintPlan* plan) {
-    plan->region_word.clear();
-    plan->region_blob.clear();
     plan->blob_region.assign(n_blobs + 1, 0);
+    plan->max_regions = 0;
+    uint64_t R = 0;
     for (uint64_t b = 0; b < n_blobs; ++b) {
-        plan->blob_region[b] = plan->region_word.size();
+        plan->blob_region[b] = R;
         const uint64_t s = blob_off[b], e = blob_off[b + 1];
-        if (e > s)
-            for (uint64_t a = s / kRegionBytes * kRegionBytes; a < e; a += kRegionBytes) {
-                plan->region_word.push_back(a / 16);
-                plan->region_blob.push_back((uint32_t)b);
-            }
+        const uint64_t nr = e > s ? (e - 1) / kRegionBytes - s / kRegionBytes + 1 : 0;
+        R += nr;
+        if (nr > plan->max_regions) plan->max_regions = nr;
     }
-    plan->blob_region[n_blobs] = plan->region_word.size();
-}
-
-size_t varint_plan_device_bytes(const VarintPlan& p, uint64_t n_blobs) {
-    const size_t R = p.region_word.size();
-    return 64 * 8 + R * (8 + 4 + 4 + 8) + (n_blobs + 1) * (8 + 8) + n_blobs * (4 + 8);
+    plan->blob_region[n_blobs] = R;
+    plan->regions = R;
 }
 
 // Layout of the device workspace for the decode passes.
 struct DecodeWork {
-    uint64_t* region_word; uint32_t* region_blob; uint32_t* region_count; uint64_t* region_base;
+    uint32_t* region_count; uint64_t* region_base;
     uint64_t* blob_off; uint64_t* blob_region; uint32_t* irregular; uint64_t* blob_count;
 };
 static DecodeWork carve(void* work, size_t R, uint64_t n_blobs) {
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     char* p = static_cast<char*>(work);
     DecodeWork w;
-    w.region_word = (uint64_t*)p; p += up(R * 8);
     w.region_base = (uint64_t*)p; p += up(R * 8);
-    w.region_blob = (uint32_t*)p; p += up(R * 4);
     w.region_count = (uint32_t*)p; p += up(R * 4);
     w.blob_off = (uint64_t*)p; p += up((n_blobs + 1) * 8);
     w.blob_region = (uint64_t*)p; p += up((n_blobs + 1) * 8);
@@ -354,23 +401,22 @@ static DecodeWork carve(void* work, size_t R, uint64_t n_blobs) {
     return w;
 }
 size_t varint_decode_work_bytes(size_t regions, uint64_t n_blobs) {
-    return 8 * 256 + regions * 24 + (n_blobs + 1) * 16 + n_blobs * 12 + 4096;
+    return regions * 12 + (n_blobs + 1) * 16 + n_blobs * 12 + 8 * 256;
 }
 
 hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
                                const VarintPlan& plan, void* work, uint64_t* counts_host, bool* irregular_any,
                                hipStream_t s) {
-    const size_t R = plan.region_word.size();
+    const size_t R = plan.regions;
     DecodeWork w = carve(work, R, n_blobs);
     hipError_t e;
-    if (R && (e = hipMemcpyAsync(w.region_word, plan.region_word.data(), R * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if (R && (e = hipMemcpyAsync(w.region_blob, plan.region_blob.data(), R * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     if ((e = hipMemcpyAsync(w.blob_off, blob_off_host, (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     if ((e = hipMemcpyAsync(w.blob_region, plan.blob_region.data(), (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.irregular, 0, n_blobs * 4, s)) != hipSuccess) return e;
-    if (R) {
-        hipLaunchKernelGGL(varint_count_kernel, dim3((unsigned)R), dim3(kThreads), 0, s, bytes, w.region_word,
-                           w.region_blob, w.blob_off, w.region_count, w.irregular);
+    for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
+        const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
+        hipLaunchKernelGGL(varint_count_kernel, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s, bytes,
+                           w.blob_region, w.blob_off, (uint32_t)y0, w.region_count, w.irregular);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(varint_scan_kernel, dim3((unsigned)n_blobs), dim3(kThreads), 0, s, w.region_count,
@@ -391,12 +437,13 @@ hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_ho
 hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
                                 int64_t* out, uint64_t out_stride, uint64_t len, bool irregular_any,
                                 hipStream_t s) {
-    const size_t R = plan.region_word.size();
+    const size_t R = plan.regions;
     DecodeWork w = carve(work, R, n_blobs);
     hipError_t e;
-    if (R) {
-        hipLaunchKernelGGL(varint_decode_kernel, dim3((unsigned)R), dim3(kThreads), 0, s, bytes, w.region_word,
-                           w.region_blob, w.blob_off, w.region_base, w.irregular, out, out_stride);
+    for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
+        const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
+        hipLaunchKernelGGL(varint_decode_kernel, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s, bytes,
+                           w.blob_region, w.blob_off, (uint32_t)y0, w.region_base, w.irregular, out, out_stride);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (irregular_any) {

@@ -613,7 +613,7 @@ sda_status codec_count(sda_engine* h, const uint8_t* bytes, const uint64_t* blob
         if (blob_off[b + 1] < blob_off[b]) return fail(SDA_ERR_INVALID_ARGUMENT, "blob offsets must be non-decreasing");
     sda::varint_plan(blob_off, n_blobs, plan);
     if (sda_status e = ensure(&h->codec_work, &h->codec_work_bytes,
-                              sda::varint_decode_work_bytes(plan->region_word.size(), n_blobs)))
+                              sda::varint_decode_work_bytes(plan->regions, n_blobs)))
         return e;
     HIP_TRY(sda::launch_varint_count(bytes, blob_off, n_blobs, *plan, h->codec_work, counts, irregular, st));
     return SDA_OK;

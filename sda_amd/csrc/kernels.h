@@ -68,9 +68,9 @@ hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indic
 // Host-side plan of the decode: blobs are split into 4 KiB regions aligned to the (16-byte
 // aligned) byte buffer; a region shared by two blobs appears once per blob.
 struct VarintPlan {
-    std::vector<uint64_t> region_word;   // first 16-byte word of the region
-    std::vector<uint32_t> region_blob;   // blob it is decoded for
-    std::vector<uint64_t> blob_region;   // [n_blobs + 1] first region of each blob
+    std::vector<uint64_t> blob_region;   // [n_blobs + 1] first region of each blob (prefix sum)
+    uint64_t regions = 0;
+    uint64_t max_regions = 0;            // regions of the largest blob (grid.x)
 };
 void varint_plan(const uint64_t* blob_off, uint64_t n_blobs, VarintPlan* plan);
 size_t varint_decode_work_bytes(size_t regions, uint64_t n_blobs);
