@@ -223,6 +223,40 @@ sda_status sda_varint_encode_dev(sda_engine* h, const int64_t* vals, uint64_t ro
                                  uint64_t stride, uint8_t* dst, uint64_t dst_cap,
                                  uint64_t* row_bytes, void* stream);
 
+/* ---------------- fused role pipelines ---------------- */
+
+/* Recipient reveal (receive.rs:80-157) + RecipientOutput::positive (:14-20) as one device
+ * pipeline: mask combine -> reconstruct -> fused unmask+positive, no host round trip between.
+ *   mask_in: Full = masks [n_masks][mask_width] i64; ChaCha = seeds [n_masks][mask_width] u32
+ *            (1..8 words); None = n_masks rows of width 0.
+ *   shares [n_idx][share_len] at clerk `indices` (host array); dimension = the reconstructor's
+ *   factory argument (vector_dimension); output_modulus = aggregation.modulus for positive().
+ *   Errors as the reference: Not enough shares (6), Mismatching dimension (4), assert -> 64. */
+sda_status sda_recipient_reveal_dev(sda_engine* h, const sda_masking_scheme* ms, const void* mask_in,
+                                    uint64_t n_masks, uint64_t mask_width, const sda_sharing_scheme* ss,
+                                    uint64_t dimension, const uint64_t* indices, const int64_t* shares,
+                                    uint64_t n_idx, uint64_t share_len, int64_t output_modulus,
+                                    int32_t mode, int64_t* out, uint64_t out_cap, uint64_t* out_len,
+                                    void* stream);
+/* Host form: mask rows as MaskCombiner::combine takes them (Full masks / ChaCha seeds-as-i64),
+ * share rows as SecretReconstructor::reconstruct takes them. */
+sda_status sda_recipient_reveal(sda_engine* h, const sda_masking_scheme* ms,
+                                const int64_t* const* mask_rows, const uint64_t* mask_lens, uint64_t n_masks,
+                                const sda_sharing_scheme* ss, uint64_t dimension, const uint64_t* indices,
+                                const int64_t* const* share_rows, const uint64_t* share_lens, uint64_t n_idx,
+                                int64_t output_modulus, int32_t mode,
+                                int64_t* out, uint64_t out_cap, uint64_t* out_len);
+
+/* Participant (participate.rs:53-76): SecretMasker::mask -> ShareGenerator::generate -> per-clerk
+ * payload encoding (sodium.rs:36-41) on device.  seed: host words (ChaCha); full_masks: device [D]
+ * (Full); secrets [D], draws (as sda_share_generate) and shares_out [n][B] are device buffers.
+ * payload (device, may be NULL): the n clerk payloads back to back, payload_row_bytes[n] (host). */
+sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms, const uint32_t* seed,
+                                     uint64_t seed_words, const int64_t* full_masks,
+                                     const sda_sharing_scheme* ss, const int64_t* secrets, uint64_t dimension,
+                                     const int64_t* draws, int64_t* shares_out, uint8_t* payload,
+                                     uint64_t payload_cap, uint64_t* payload_row_bytes, void* stream);
+
 /* Synthetic benchmark input: dst[r*cols + c] = lo + splitmix64(seed, r, c) % (hi - lo). */
 sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64_t cols,
                               uint64_t seed, int64_t lo, int64_t hi, void* stream);

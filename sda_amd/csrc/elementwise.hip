@@ -44,6 +44,19 @@ __global__ __launch_bounds__(256) void positive_kernel(const int64_t* __restrict
     out[i] = x < 0 ? (int64_t)((uint64_t)x + (uint64_t)m) : x;
 }
 
+// recipient epilogue (receive.rs:149-157 + :14-20): out = positive((ms - mask) % q) in one pass;
+// mask == nullptr (None masking, none.rs:28-32) skips the unmask, pos_m == 0 skips positive().
+__global__ __launch_bounds__(256) void unmask_positive_kernel(const int64_t* __restrict__ ms,
+                                                              const int64_t* __restrict__ mask, uint64_t D,
+                                                              Mod64 Q, int64_t pos_m, int64_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= D) return;
+    int64_t x = ms[i];
+    if (mask) x = trem64((int64_t)((uint64_t)x - (uint64_t)mask[i]), Q);
+    if (pos_m && x < 0) x = (int64_t)((uint64_t)x + (uint64_t)pos_m);
+    out[i] = x;
+}
+
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t idx) {
     uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -83,6 +96,14 @@ hipError_t launch_addsub_trem(const int64_t* a, const int64_t* b, int sign, uint
 hipError_t launch_positive(const int64_t* v, uint64_t D, int64_t* out, int64_t modulus, hipStream_t s) {
     if (D == 0) return hipSuccess;
     hipLaunchKernelGGL(positive_kernel, dim3(grid_for(D)), dim3(256), 0, s, v, D, out, modulus);
+    return hipGetLastError();
+}
+
+hipError_t launch_unmask_positive(const int64_t* ms, const int64_t* mask, uint64_t D, int64_t q, int64_t pos_m,
+                                  int64_t* out, hipStream_t s) {
+    if (D == 0) return hipSuccess;
+    hipLaunchKernelGGL(unmask_positive_kernel, dim3(grid_for(D)), dim3(256), 0, s, ms, mask, D,
+                       make_mod64(q > 0 ? q : 1), pos_m, out);
     return hipGetLastError();
 }
 

@@ -31,6 +31,8 @@ struct sda_engine {
     size_t codec_work_bytes = 0;
     void* codec_mat = nullptr;    // decoded [N][len] matrix of the clerk decode+combine path
     size_t codec_mat_bytes = 0;
+    void* pipe = nullptr;         // recipient / participant pipeline scratch (mask, masked, compacted shares)
+    size_t pipe_bytes = 0;
     sda::DeviceTable rev_tab;     // packed-Shamir Newton/Lagrange tables (per scheme + clerk set)
 };
 
@@ -202,6 +204,7 @@ void sda_engine_destroy(sda_engine* h) {
     if (h->gen_log) (void)hipFree(h->gen_log);
     if (h->codec_work) (void)hipFree(h->codec_work);
     if (h->codec_mat) (void)hipFree(h->codec_mat);
+    if (h->pipe) (void)hipFree(h->pipe);
     if (h->stage) (void)hipFree(h->stage);
     sda::free_table(h->gen_tab);
     sda::free_table(h->rev_tab);
@@ -774,6 +777,245 @@ sda_status sda_varint_encode_dev(sda_engine* h, const int64_t* vals, uint64_t ro
                                              pick(h, stream));
     if (e == hipErrorInvalidValue) return fail(SDA_ERR_INVALID_ARGUMENT, "dst_cap too small");
     HIP_TRY(e);
+    return ok();
+}
+
+}  // extern "C"
+
+// ---------------- fused role pipelines ----------------
+namespace {
+
+// receive.rs:80-157 + :14-20 on device-resident inputs (see sda_recipient_reveal_dev).
+sda_status recipient_pipeline(sda_engine* h, const sda_masking_scheme* ms, const void* mask_in, uint64_t n_masks,
+                              uint64_t mask_width, const sda_sharing_scheme* ss, uint64_t dimension,
+                              const uint64_t* indices, const int64_t* shares, uint64_t n_idx, uint64_t share_len,
+                              int64_t output_modulus, int32_t mode, int64_t* out, uint64_t out_cap,
+                              uint64_t* out_len, hipStream_t st) {
+    *out_len = 0;
+    // ---- masked output length (reconstruct) ----
+    uint64_t D;
+    if (ss->kind == SDA_SHARING_ADDITIVE) {
+        D = n_idx ? share_len : 0;                           // additive.rs:56-60
+    } else if (ss->kind == SDA_SHARING_PACKED_SHAMIR) {
+        if (sda_status e = check_packed(ss)) return e;
+        if (n_idx < ss->privacy_threshold + ss->secret_count)
+            return fail(SDA_ERR_NOT_ENOUGH_SHARES, "Not enough shares to reconstruct");   // packed_shamir.rs:75
+        if (n_idx > 63) return fail(SDA_ERR_UNSUPPORTED, "more than 63 clerk shares per batch");
+        if (mode != SDA_REVEAL_EXACT && mode != SDA_REVEAL_CANONICAL) return fail(SDA_ERR_INVALID_ARGUMENT, "bad mode");
+        const uint64_t B = (dimension + ss->secret_count - 1) / ss->secret_count;
+        if (dimension && share_len < B)
+            return fail(SDA_ERR_PRECONDITION, "index out of bounds: clerk vector shorter than the batch count");
+        D = dimension;
+    } else {
+        return fail(SDA_ERR_INVALID_ARGUMENT, "unknown sharing scheme kind");
+    }
+    // ---- mask length (mask combine) ----
+    uint64_t mask_len = 0;
+    if (ms->kind == SDA_MASKING_NONE) {
+        if (n_masks && mask_width) return fail(SDA_ERR_PRECONDITION, "assertion failed: masks.iter().all(|mask| mask.len() == 0)");
+    } else if (ms->kind == SDA_MASKING_FULL) {
+        mask_len = n_masks ? mask_width : 0;                // full.rs:40
+    } else if (ms->kind == SDA_MASKING_CHACHA) {
+        mask_len = ms->dimension;                           // chacha.rs:58
+        if (mask_width == 0 || mask_width > 8) return fail(SDA_ERR_UNSUPPORTED, "device seeds must be 1..8 words");
+    } else {
+        return fail(SDA_ERR_INVALID_ARGUMENT, "unknown masking scheme kind");
+    }
+    if (ms->kind != SDA_MASKING_NONE && mask_len != D)     // chacha.rs:83 / full.rs:58 assert_eq!
+        return fail(SDA_ERR_PRECONDITION, "assertion failed: mask.len() == masked_secrets.len() (%llu vs %llu)",
+                    (unsigned long long)mask_len, (unsigned long long)D);
+    if (out_cap < D) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
+    if (D == 0) return ok();
+    int64_t q = 1;
+    if (ms->kind != SDA_MASKING_NONE)
+        if (sda_status e = modulus_abs(ms->modulus, &q)) return e;
+    const bool packed = ss->kind == SDA_SHARING_PACKED_SHAMIR;
+    const uint64_t B = packed ? (dimension + ss->secret_count - 1) / ss->secret_count : 0;
+    const bool compact = packed && share_len != B;
+    if (sda_status e = ensure(&h->pipe, &h->pipe_bytes, 2 * rup(D * 8) + (compact ? rup(n_idx * B * 8) : 0) + 256))
+        return e;
+    int64_t* dmask = static_cast<int64_t*>(h->pipe);
+    int64_t* dmasked = dmask + rup(D * 8) / 8;
+    // 1. masks (receive.rs:101-117)
+    if (ms->kind == SDA_MASKING_FULL) {
+        if (sda_status e = modulus_abs(ms->modulus, &q)) return e;
+        HIP_TRY(sda::launch_combine_exact(static_cast<const int64_t*>(mask_in), n_masks, D, mask_width, dmask, q, st));
+    } else if (ms->kind == SDA_MASKING_CHACHA) {
+        if (ms->modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
+        if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D))) return e;
+        int fixups = 0;
+        HIP_TRY(sda::launch_chacha_mask_combine(ms->modulus, D, static_cast<const uint32_t*>(mask_in),
+                                                (uint32_t)mask_width, n_masks, dmask, h->work, st, &fixups));
+    }
+    // 2. reconstruct (receive.rs:120-146)
+    if (!packed) {
+        int64_t m;
+        if (sda_status e = modulus_abs(ss->modulus, &m)) return e;
+        HIP_TRY(sda::launch_combine_exact(shares, n_idx, D, share_len, dmasked, m, st));
+    } else {
+        const int64_t* src = shares;
+        if (compact) {                                      // batched.rs:83-85 reads [clerk][0..B)
+            int64_t* c = dmasked + rup(D * 8) / 8;
+            HIP_TRY(hipMemcpy2DAsync(c, B * 8, shares, share_len * 8, B * 8, n_idx, hipMemcpyDeviceToDevice, st));
+            src = c;
+        }
+        sda::PackedRevealArgs ra{src, dimension, 1, dmasked};
+        hipError_t e = sda::launch_packed_reveal(ra, indices, (uint32_t)n_idx, (uint32_t)ss->secret_count,
+                                                 (uint32_t)ss->modulus, (uint32_t)ss->omega_secrets,
+                                                 (uint32_t)ss->omega_shares, mode, h->rev_tab, st);
+        if (e == hipErrorInvalidValue && mode == SDA_REVEAL_CANONICAL)
+            return fail(SDA_ERR_UNSUPPORTED, "canonical reveal needs distinct clerk indices");
+        HIP_TRY(e);
+    }
+    // 3. unmask (receive.rs:149-152) + RecipientOutput::positive (:14-20), one pass
+    HIP_TRY(sda::launch_unmask_positive(dmasked, ms->kind == SDA_MASKING_NONE ? nullptr : dmask, D, q,
+                                        output_modulus, out, st));
+    *out_len = D;
+    return SDA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+sda_status sda_recipient_reveal_dev(sda_engine* h, const sda_masking_scheme* ms, const void* mask_in, uint64_t n_masks,
+                                    uint64_t mask_width, const sda_sharing_scheme* ss, uint64_t dimension,
+                                    const uint64_t* indices, const int64_t* shares, uint64_t n_idx,
+                                    uint64_t share_len, int64_t output_modulus, int32_t mode, int64_t* out,
+                                    uint64_t out_cap, uint64_t* out_len, void* stream) {
+    if (!h || !ms || !ss || !out_len || (n_idx && (!shares || !indices)) || (n_masks && mask_width && !mask_in))
+        return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    HIP_TRY(hipSetDevice(h->device));
+    if (sda_status e = recipient_pipeline(h, ms, mask_in, n_masks, mask_width, ss, dimension, indices, shares, n_idx,
+                                          share_len, output_modulus, mode, out, out_cap, out_len, pick(h, stream)))
+        return e;
+    return ok();
+}
+
+sda_status sda_recipient_reveal(sda_engine* h, const sda_masking_scheme* ms, const int64_t* const* mask_rows,
+                                const uint64_t* mask_lens, uint64_t n_masks, const sda_sharing_scheme* ss,
+                                uint64_t dimension, const uint64_t* indices, const int64_t* const* share_rows,
+                                const uint64_t* share_lens, uint64_t n_idx, int64_t output_modulus, int32_t mode,
+                                int64_t* out, uint64_t out_cap, uint64_t* out_len) {
+    if (!h || !ms || !ss || !out_len || (n_masks && (!mask_rows || !mask_lens)) ||
+        (n_idx && (!share_rows || !share_lens || !indices)))
+        return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    *out_len = 0;
+    HIP_TRY(hipSetDevice(h->device));
+    // host-side shape checks in the reference's order, then one upload
+    uint64_t share_len = n_idx ? share_lens[0] : 0;
+    for (uint64_t i = 0; i < n_idx; ++i) {
+        if (share_lens[i] == share_len) continue;
+        if (ss->kind == SDA_SHARING_ADDITIVE) return fail(SDA_ERR_MISMATCHING_DIMENSION, "Mismatching dimension");
+        share_len = share_lens[i] < share_len ? share_lens[i] : share_len;   // packed: reads [0, B) of each
+    }
+    uint64_t width = 0;
+    std::vector<uint32_t> seeds;
+    if (ms->kind == SDA_MASKING_FULL) {
+        width = n_masks ? mask_lens[0] : 0;
+        for (uint64_t i = 0; i < n_masks; ++i)
+            if (mask_lens[i] != width) return fail(SDA_ERR_PRECONDITION, "assertion failed: mask.len() == dimension");
+    } else if (ms->kind == SDA_MASKING_CHACHA) {
+        for (uint64_t i = 0; i < n_masks; ++i) width = mask_lens[i] > width ? mask_lens[i] : width;
+        width = width > 8 ? 8 : (width == 0 ? 1 : width);    // key = first 8 words, zero padded
+        seeds.assign(n_masks * width, 0u);
+        for (uint64_t i = 0; i < n_masks; ++i)
+            for (uint64_t j = 0; j < mask_lens[i] && j < width; ++j) seeds[i * width + j] = (uint32_t)mask_rows[i][j];
+    } else {
+        for (uint64_t i = 0; i < n_masks; ++i)
+            if (mask_lens[i]) return fail(SDA_ERR_PRECONDITION, "assertion failed: masks.iter().all(|mask| mask.len() == 0)");
+    }
+    const uint64_t outn = ss->kind == SDA_SHARING_ADDITIVE ? share_len : dimension;
+    DevArena a;
+    if (sda_status e = stage(h, rup(n_idx * share_len * 8 + 8) + rup(n_masks * width * 8 + 8) + rup(outn * 8 + 8), &a))
+        return e;
+    int64_t* dsh = a.take<int64_t>(n_idx * share_len + 1);
+    void* dmask = a.take<int64_t>(n_masks * width + 1);
+    int64_t* dout = a.take<int64_t>(outn + 1);
+    for (uint64_t i = 0; i < n_idx; ++i)
+        if (share_len) HIP_TRY(hipMemcpyAsync(dsh + i * share_len, share_rows[i], share_len * 8, hipMemcpyHostToDevice, h->stream));
+    if (ms->kind == SDA_MASKING_FULL)
+        for (uint64_t i = 0; i < n_masks; ++i)
+            if (width) HIP_TRY(hipMemcpyAsync(static_cast<int64_t*>(dmask) + i * width, mask_rows[i], width * 8,
+                                              hipMemcpyHostToDevice, h->stream));
+    if (ms->kind == SDA_MASKING_CHACHA && !seeds.empty())
+        HIP_TRY(hipMemcpyAsync(dmask, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, h->stream));
+    uint64_t len = 0;
+    if (sda_status e = recipient_pipeline(h, ms, dmask, n_masks, ms->kind == SDA_MASKING_NONE ? 0 : width, ss,
+                                          dimension, indices, dsh, n_idx, share_len, output_modulus, mode, dout,
+                                          (uint64_t)-1, &len, h->stream))
+        return e;
+    if (out_cap < len) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
+    if (len) HIP_TRY(hipMemcpyAsync(out, dout, len * 8, hipMemcpyDeviceToHost, h->stream));
+    *out_len = len;
+    return finish(h);
+}
+
+// participate.rs:53-76 (+ the encoding step of Encryptor::encrypt, sodium.rs:36-41) on device.
+sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms, const uint32_t* seed,
+                                     uint64_t seed_words, const int64_t* full_masks, const sda_sharing_scheme* ss,
+                                     const int64_t* secrets, uint64_t dimension, const int64_t* draws,
+                                     int64_t* shares_out, uint8_t* payload, uint64_t payload_cap,
+                                     uint64_t* payload_row_bytes, void* stream) {
+    if (!h || !ms || !ss || (dimension && (!secrets || !shares_out)) || (payload && !payload_row_bytes))
+        return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = pick(h, stream);
+    const uint64_t D = dimension;
+    const bool packed = ss->kind == SDA_SHARING_PACKED_SHAMIR;
+    if (!packed && ss->kind != SDA_SHARING_ADDITIVE) return fail(SDA_ERR_INVALID_ARGUMENT, "unknown sharing scheme kind");
+    if (packed) {
+        if (sda_status e = check_packed(ss)) return e;
+    } else {
+        if (ss->share_count == 0) return fail(SDA_ERR_PRECONDITION, "share_count - 1 underflows (additive.rs:42)");
+        if (ss->modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
+    }
+    // 1. SecretMasker::mask (participate.rs:53-54)
+    const int64_t* masked = secrets;
+    if (ms->kind != SDA_MASKING_NONE && D) {
+        if (ms->modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
+        if (sda_status e = ensure(&h->pipe, &h->pipe_bytes, rup(D * 8) + 256)) return e;
+        int64_t* dm = static_cast<int64_t*>(h->pipe);
+        if (ms->kind == SDA_MASKING_FULL) {
+            if (!full_masks) return fail(SDA_ERR_INVALID_ARGUMENT, "Full masking needs the drawn masks");
+            HIP_TRY(sda::launch_addsub_trem(secrets, full_masks, +1, D, dm, ms->modulus, st));      // full.rs:28-31
+        } else if (ms->kind == SDA_MASKING_CHACHA) {
+            if (ms->dimension != D) return fail(SDA_ERR_PRECONDITION, "assertion failed: dimension == secrets.len()");
+            const uint64_t want = (ms->seed_bitsize + 31) / 32;
+            if (seed_words != want || (seed_words && !seed))
+                return fail(SDA_ERR_PRECONDITION, "expected %llu seed words", (unsigned long long)want);
+            if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D) + 64 + D * 8)) return e;
+            HIP_TRY(sda::launch_chacha_mask(ms->modulus, seed, (uint32_t)(seed_words < 8 ? seed_words : 8), secrets, D,
+                                            dm, h->work, st));                                       // chacha.rs:36-45
+        } else {
+            return fail(SDA_ERR_INVALID_ARGUMENT, "unknown masking scheme kind");
+        }
+        masked = dm;
+    }
+    // 2. ShareGenerator::generate (participate.rs:75-76): shares [n][B]
+    const uint64_t n = ss->share_count;
+    const uint64_t B = packed ? (D + ss->secret_count - 1) / ss->secret_count : D;
+    if (B) {
+        if (!draws) return fail(SDA_ERR_INVALID_ARGUMENT, "need the randomness draws");
+        if (packed) {
+            if (sda_status e = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return e;
+            sda::PackedGenArgs ga{masked, D, 1, draws, shares_out};
+            HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)ss->secret_count, (uint32_t)ss->privacy_threshold,
+                                                (uint32_t)n, (uint32_t)ss->modulus, (uint32_t)ss->omega_secrets,
+                                                (uint32_t)ss->omega_shares, h->gen_tab, h->gen_log, st));
+        } else {
+            HIP_TRY(sda::launch_additive_generate(masked, D, draws, n, shares_out, ss->modulus, st));
+        }
+    }
+    // 3. per-clerk payload encoding (participate.rs:79-98 -> sodium.rs:36-41); sealing stays on the host
+    if (payload) {
+        if (n > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 clerks");
+        if (sda_status e = ensure(&h->codec_work, &h->codec_work_bytes, sda::varint_encode_work_bytes(n, B))) return e;
+        hipError_t e = sda::launch_varint_encode(shares_out, n, B, B, payload, payload_cap, h->codec_work,
+                                                 payload_row_bytes, st);
+        if (e == hipErrorInvalidValue) return fail(SDA_ERR_INVALID_ARGUMENT, "payload_cap too small");
+        HIP_TRY(e);
+    }
     return ok();
 }
 

@@ -26,6 +26,9 @@ hipError_t launch_addsub_trem(const int64_t* a, const int64_t* b, int sign, uint
                               int64_t* out, int64_t modulus, hipStream_t s);
 hipError_t launch_positive(const int64_t* v, uint64_t D, int64_t* out, int64_t modulus,
                            hipStream_t s);
+// out = positive((ms - mask) % q, pos_m); mask == nullptr: no unmask; pos_m == 0: no positive()
+hipError_t launch_unmask_positive(const int64_t* ms, const int64_t* mask, uint64_t D, int64_t q, int64_t pos_m,
+                                  int64_t* out, hipStream_t s);
 hipError_t launch_synth_fill(int64_t* dst, uint64_t rows, uint64_t cols, uint64_t seed,
                              int64_t lo, int64_t hi, hipStream_t s);
 

@@ -91,6 +91,15 @@ SIGNATURES = [
     ("sda_varint_decode_dev", _st, [_vp, _vp, _u64p, C.c_uint64, _vp, C.c_uint64, _u64p, _vp]),
     ("sda_clerk_decode_combine_dev", _st, [_vp, C.c_int64, _vp, _u64p, C.c_uint64, _vp, C.c_uint64, _u64p, _vp]),
     ("sda_varint_encode_dev", _st, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp, C.c_uint64, _u64p, _vp]),
+    ("sda_recipient_reveal_dev", _st, [_vp, C.POINTER(S.MaskingSchemeC), _vp, C.c_uint64, C.c_uint64,
+                                       C.POINTER(S.SharingSchemeC), C.c_uint64, _u64p, _vp, C.c_uint64, C.c_uint64,
+                                       C.c_int64, C.c_int32, _vp, C.c_uint64, _u64p, _vp]),
+    ("sda_recipient_reveal", _st, [_vp, C.POINTER(S.MaskingSchemeC), C.POINTER(_i64p), _u64p, C.c_uint64,
+                                   C.POINTER(S.SharingSchemeC), C.c_uint64, _u64p, C.POINTER(_i64p), _u64p,
+                                   C.c_uint64, C.c_int64, C.c_int32, _i64p, C.c_uint64, _u64p]),
+    ("sda_participant_share_dev", _st, [_vp, C.POINTER(S.MaskingSchemeC), _u32p, C.c_uint64, _vp,
+                                        C.POINTER(S.SharingSchemeC), _vp, C.c_uint64, _vp, _vp, _vp, C.c_uint64,
+                                        _u64p, _vp]),
 ]
 
 _lib = None
@@ -262,6 +271,22 @@ class Engine:
                                                  C.byref(olen)))
         return out[: olen.value]
 
+    # ---------------- fused role pipelines ----------------
+    def recipient_reveal(self, masking, mask_rows, sharing, dimension: int, indexed_shares, output_modulus: int,
+                         mode=REVEAL_EXACT) -> np.ndarray:
+        """receive.rs:80-157 + positive() (:14-20) as one device pipeline."""
+        ms, ss = masking.c(), sharing.c()
+        marrs, mptrs, mlens, nm = _rows(mask_rows)
+        idx = _arr([i for i, _ in indexed_shares], np.uint64)
+        sarrs, sptrs, slens, ns = _rows([r for _, r in indexed_shares])
+        cap = max(dimension, sarrs[0].size if sarrs else 0, 1)
+        out = np.zeros(cap, np.int64)
+        olen = C.c_uint64(0)
+        _check(self.lib.sda_recipient_reveal(self.h, C.byref(ms), mptrs, mlens, nm, C.byref(ss), dimension,
+                                             _ptr(idx, _u64p), sptrs, slens, ns, output_modulus, mode, _ptr(out),
+                                             out.size, C.byref(olen)))
+        return out[: olen.value]
+
     def synchronize(self):
         _check(self.lib.sda_engine_synchronize(self.h))
 
@@ -315,3 +340,25 @@ class Engine:
         _check(self.lib.sda_varint_encode_dev(self.h, vals_ptr, rows, length, stride, dst_ptr, dst_cap,
                                               _ptr(rb, _u64p), stream))
         return rb[:rows]
+
+    def recipient_reveal_dev(self, masking, mask_ptr, n_masks, mask_width, sharing, dimension, indices, shares_ptr,
+                             share_len, output_modulus, out_ptr, out_cap, mode=REVEAL_EXACT, stream=None) -> int:
+        ms, ss = masking.c(), sharing.c()
+        idx = _arr(indices, np.uint64)
+        olen = C.c_uint64(0)
+        _check(self.lib.sda_recipient_reveal_dev(self.h, C.byref(ms), mask_ptr, n_masks, mask_width, C.byref(ss),
+                                                 dimension, _ptr(idx, _u64p), shares_ptr, idx.size, share_len,
+                                                 output_modulus, mode, out_ptr, out_cap, C.byref(olen), stream))
+        return olen.value
+
+    def participant_share_dev(self, masking, sharing, secrets_ptr, dimension, draws_ptr, shares_ptr, seed=None,
+                              full_masks_ptr=None, payload_ptr=None, payload_cap=0, stream=None):
+        """participate.rs:53-76 (+ payload encoding) on device; returns per-clerk payload byte counts."""
+        ms, ss = masking.c(), sharing.c()
+        sd = _arr(seed if seed is not None else [], np.uint32)
+        n = sharing.output_size()
+        rb = np.zeros(max(n, 1), np.uint64)
+        _check(self.lib.sda_participant_share_dev(self.h, C.byref(ms), _ptr(sd, _u32p), sd.size, full_masks_ptr,
+                                                  C.byref(ss), secrets_ptr, dimension, draws_ptr, shares_ptr,
+                                                  payload_ptr, payload_cap, _ptr(rb, _u64p), stream))
+        return rb[:n]
