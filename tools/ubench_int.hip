@@ -26,7 +26,10 @@ __global__ __launch_bounds__(256) void ubench(uint32_t seed, uint64_t* sink) {
         if constexpr (OP == 6) asm volatile("v_min_u32 %0, %0, %1" : "+v"(a##i) : "v"(b));             \
         if constexpr (OP == 7) asm volatile("v_cmp_gt_u32 vcc, %0, %1\n\tv_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##i) : "v"(b) : "vcc"); \
         if constexpr (OP == 8) asm volatile("v_lshl_add_u64 %0, %0, 1, %0" : "+v"(w##i));              \
-        if constexpr (OP == 9) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a##i) : "v"(b));
+        if constexpr (OP == 9) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a##i) : "v"(b));            \
+        if constexpr (OP == 10) asm volatile("v_perm_b32 %0, %0, %0, %1" : "+v"(a##i) : "v"(b));      \
+        if constexpr (OP == 11) asm volatile("v_alignbit_b32 %0, %0, %0, 16" : "+v"(a##i));             \
+        if constexpr (OP == 12) asm volatile("v_xad_u32 %0, %0, %1, %0" : "+v"(a##i) : "v"(b));
         REP8(STEP)
     }
     uint64_t s = (uint64_t)a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + w0 + w1 + w2 + w3 + w4 + w5 + w6 + w7;
@@ -63,6 +66,10 @@ int main() {
     run<3>("v_mad_u64_u32", sink, 1);
     run<4>("v_mad_i64_i32", sink, 1);
     run<8>("v_lshl_add_u64", sink, 1);
+    run<10>("v_perm_b32", sink, 1);
+    run<11>("v_alignbit_b32 (16)", sink, 1);
+    run<12>("v_xad_u32", sink, 1);
+    run<0>("v_add_u32 (again)", sink, 1);
     (void)hipFree(sink);
     return 0;
 }
