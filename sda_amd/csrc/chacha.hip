@@ -60,11 +60,16 @@ struct RejectLog {
     uint64_t cap;
 };
 
-// acc[i] += sum over seeds in this y-chunk of draw_i  (un-shifted), canonical per chunk
+// acc[i] += sum over seeds in this y-chunk of draw_i  (un-shifted), canonical per chunk.
+// Every draw is >= 0, so the reference's running `(r + draw) % m` equals (sum of draws) mod m.
+// LAZY (m <= 2^32): the raw 64-bit words v are summed into 96-bit accumulators (3 adds per draw)
+// and reduced once per chunk -- (sum of v) mod m == sum of (v mod m) mod m; otherwise each draw
+// is reduced with the 64-bit Barrett `%`.
+template <bool LAZY>
 __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __restrict__ seeds, uint32_t w,
                                                              uint64_t n_seeds, uint64_t seeds_per_chunk,
                                                              uint64_t D, unsigned long long* __restrict__ acc,
-                                                             Mod64 M, uint64_t zone, RejectLog log) {
+                                                             Mod64 M, uint64_t zone, uint64_t r64, RejectLog log) {
     const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t n_blk = (D + 7) / 8;
     if (blk >= n_blk) return;
@@ -72,9 +77,11 @@ __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __r
     const uint64_t s1 = s0 + seeds_per_chunk < n_seeds ? s0 + seeds_per_chunk : n_seeds;
     const uint32_t nw = w < 8 ? w : 8;
     const uint64_t m = M.m;
+    const uint32_t nvalid = D - blk * 8 < 8 ? (uint32_t)(D - blk * 8) : 8u;   // pairs of this block inside D
     uint64_t a[8];
+    uint32_t hi[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) a[q] = 0;
+    for (int q = 0; q < 8; ++q) { a[q] = 0; hi[q] = 0; }
     for (uint64_t s = s0; s < s1; ++s) {
         uint32_t key[8];
 #pragma unroll
@@ -84,20 +91,33 @@ __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __r
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const uint64_t v = ((uint64_t)o[2 * q] << 32) | o[2 * q + 1];    // high word first
-            const uint64_t pair = blk * 8 + q;
-            if (pair < D) {
+            if ((uint32_t)q < nvalid) {
                 if (v >= zone) {                                            // rejected: log it
                     const unsigned long long slot = atomicAdd(log.count, 1ull);
-                    if (slot < log.cap) { log.seed_of[slot] = (uint32_t)s; log.pair_of[slot] = pair; }
+                    if (slot < log.cap) { log.seed_of[slot] = (uint32_t)s; log.pair_of[slot] = blk * 8 + q; }
                 }
-                uint64_t x = a[q] + umod64(v, M);
-                a[q] = x >= m ? x - m : x;
+                if constexpr (LAZY) {
+                    const uint64_t x = a[q] + v;
+                    hi[q] += x < v ? 1u : 0u;
+                    a[q] = x;
+                } else {
+                    uint64_t x = a[q] + umod64(v, M);
+                    a[q] = x >= m ? x - m : x;
+                }
             }
         }
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-        if (blk * 8 + q < D) atomicAdd(&acc[blk * 8 + q], (unsigned long long)a[q]);
+    for (int q = 0; q < 8; ++q) {
+        if ((uint32_t)q >= nvalid) continue;
+        uint64_t r = a[q];
+        if constexpr (LAZY) {       // (hi 2^64 + lo) mod m, m <= 2^32: hi mod m < m, r64 = 2^64 mod m
+            const uint64_t t = umod64((uint64_t)hi[q], M) * r64;          // < m^2 <= 2^64
+            const uint64_t x = umod64(t, M) + umod64(r, M);               // < 2m
+            r = x >= m ? x - m : x;
+        }
+        atomicAdd(&acc[blk * 8 + q], (unsigned long long)r);
+    }
 }
 
 // Fix one stream: for elements i >= i0, replace draw(pair i) by draw(pair a_i), where a_i is the
@@ -192,8 +212,15 @@ static hipError_t chacha_combine_impl(int64_t modulus, uint64_t D, const uint32_
     const uint64_t per = n_seeds ? (n_seeds + chunks - 1) / chunks : 0;
     RejectLog log{count, seed_of, pair_of, kRejectCap};
     if (n_seeds) {
-        hipLaunchKernelGGL(chacha_combine_kernel, dim3((unsigned)gx, (unsigned)chunks), dim3(256), 0, s, seeds_dev, w,
-                           n_seeds, per, D, acc, M, zone, log);
+        const uint64_t mm = (uint64_t)modulus;
+        if (mm <= (1ull << 32)) {
+            const uint64_t r64 = (UINT64_MAX % mm + 1) % mm;          // 2^64 mod m
+            hipLaunchKernelGGL(chacha_combine_kernel<true>, dim3((unsigned)gx, (unsigned)chunks), dim3(256), 0, s,
+                               seeds_dev, w, n_seeds, per, D, acc, M, zone, r64, log);
+        } else {
+            hipLaunchKernelGGL(chacha_combine_kernel<false>, dim3((unsigned)gx, (unsigned)chunks), dim3(256), 0, s,
+                               seeds_dev, w, n_seeds, per, D, acc, M, zone, (uint64_t)0, log);
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
         // read the rejection log (a few bytes) -- the call is synchronous anyway
         unsigned long long n_rej = 0;
