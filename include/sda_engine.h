@@ -158,6 +158,12 @@ sda_status sda_combine_dev(sda_engine* h, int64_t modulus, const int64_t* shares
                            uint64_t n, uint64_t dim, uint64_t row_stride,
                            int64_t* out, void* stream);
 
+/* The same recurrence continued from inout[dim] (a previous combine result, |r| < m, or zeros):
+ * a clerk job streamed through HBM in row tiles is bit-identical to one pass over all rows. */
+sda_status sda_combine_accumulate_dev(sda_engine* h, int64_t modulus, const int64_t* shares,
+                                      uint64_t n, uint64_t dim, uint64_t row_stride,
+                                      int64_t* inout, void* stream);
+
 /* Multi-GPU finalize: `sums` are the two's-complement u64 sums (RCCL-reduced) of per-GPU
  * combine results; out = canonical residue in [0, m).  Exact w.r.t. the reference when all
  * combined inputs were non-negative (DESIGN.md "multi-GPU"). */

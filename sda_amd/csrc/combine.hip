@@ -27,7 +27,9 @@ __device__ __forceinline__ int64_t lane_of(const typename vec_t<VEC>::type& v, i
     if constexpr (VEC == 1) { return v; } else { return v[e]; }
 }
 
-template <int VEC, int UNROLL, bool SMALL_M>
+// ACC: continue the recurrence from `out` (a previous combine result, |r| < m) instead of 0 --
+// a clerk job streamed through HBM in row tiles is bit-identical to one pass over all rows.
+template <int VEC, int UNROLL, bool SMALL_M, bool ACC>
 __global__ __launch_bounds__(256) void combine_exact_kernel(const int64_t* __restrict__ in,
                                                             uint64_t n, uint64_t n_lanes,
                                                             uint64_t stride,
@@ -39,7 +41,7 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const int64_t* __res
     const uint64_t vstride = stride / VEC;     // stride in units of V (host guarantees divisibility)
     int64_t r[VEC];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) r[e] = 0;
+    for (int e = 0; e < VEC; ++e) r[e] = ACC ? out[lane * VEC + e] : 0;
 
     uint64_t i = 0;
     for (; i + UNROLL <= n; i += UNROLL) {
@@ -66,16 +68,16 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const int64_t* __res
     reinterpret_cast<V*>(out)[lane] = o;
 }
 
-template <int VEC, int UNROLL>
+template <int VEC, int UNROLL, bool ACC>
 hipError_t launch_vec(const int64_t* in, uint64_t n, uint64_t dim, uint64_t stride, int64_t* out,
                       const Mod64& M, bool small_m, hipStream_t s) {
     const uint64_t n_lanes = dim / VEC;
     const uint64_t blocks = (n_lanes + 255) / 256;
     if (small_m)
-        hipLaunchKernelGGL((combine_exact_kernel<VEC, UNROLL, true>), dim3((unsigned)blocks), dim3(256), 0, s,
+        hipLaunchKernelGGL((combine_exact_kernel<VEC, UNROLL, true, ACC>), dim3((unsigned)blocks), dim3(256), 0, s,
                            in, n, n_lanes, stride, out, M);
     else
-        hipLaunchKernelGGL((combine_exact_kernel<VEC, UNROLL, false>), dim3((unsigned)blocks), dim3(256), 0, s,
+        hipLaunchKernelGGL((combine_exact_kernel<VEC, UNROLL, false, ACC>), dim3((unsigned)blocks), dim3(256), 0, s,
                            in, n, n_lanes, stride, out, M);
     return hipGetLastError();
 }
@@ -89,15 +91,18 @@ __global__ __launch_bounds__(256) void mod_canonical_kernel(const int64_t* __res
 }  // namespace
 
 hipError_t launch_combine_exact(const int64_t* in, uint64_t n, uint64_t dim, uint64_t stride,
-                                int64_t* out, int64_t modulus, hipStream_t s) {
+                                int64_t* out, int64_t modulus, hipStream_t s, bool accumulate) {
     if (dim == 0) return hipSuccess;
     const Mod64 M = make_mod64(modulus);
     const bool small_m = modulus <= ((int64_t)1 << 62);
     const uintptr_t a = (uintptr_t)in | (uintptr_t)out;
     // widest vector whose columns, row stride and base addresses all line up
-    if (dim % 2 == 0 && stride % 2 == 0 && (a % 16) == 0)
-        return launch_vec<2, 8>(in, n, dim, stride, out, M, small_m, s);
-    return launch_vec<1, 8>(in, n, dim, stride, out, M, small_m, s);
+    const bool v2 = dim % 2 == 0 && stride % 2 == 0 && (a % 16) == 0;
+    if (accumulate)
+        return v2 ? launch_vec<2, 8, true>(in, n, dim, stride, out, M, small_m, s)
+                  : launch_vec<1, 8, true>(in, n, dim, stride, out, M, small_m, s);
+    return v2 ? launch_vec<2, 8, false>(in, n, dim, stride, out, M, small_m, s)
+              : launch_vec<1, 8, false>(in, n, dim, stride, out, M, small_m, s);
 }
 
 hipError_t launch_mod_canonical(const int64_t* sums, uint64_t dim, int64_t* out, int64_t modulus,

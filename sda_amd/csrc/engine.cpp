@@ -525,6 +525,18 @@ sda_status sda_combine_dev(sda_engine* h, int64_t modulus, const int64_t* shares
     return ok();
 }
 
+sda_status sda_combine_accumulate_dev(sda_engine* h, int64_t modulus, const int64_t* shares, uint64_t n,
+                                      uint64_t dim, uint64_t row_stride, int64_t* inout, void* stream) {
+    if (!h || (dim && (!inout || (n && !shares)))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (n > 1 && row_stride < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "row_stride < dim");
+    int64_t m;
+    if (sda_status st = modulus_abs(modulus, &m)) return st;
+    HIP_TRY(hipSetDevice(h->device));
+    if (n == 0) return ok();
+    HIP_TRY(sda::launch_combine_exact(shares, n, dim, n > 1 ? row_stride : dim, inout, m, pick(h, stream), true));
+    return ok();
+}
+
 sda_status sda_combine_finalize_dev(sda_engine* h, int64_t modulus, const int64_t* sums, uint64_t dim, int64_t* out,
                                     void* stream) {
     if (!h || (dim && (!sums || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");

@@ -12,8 +12,9 @@ namespace sda {
 
 // ---- combine.hip ----
 // Exact clerk combine: out[j] = fold over rows of (r + v) % m  (combiner.rs:22-25).
+// accumulate: continue from the values in `out` (a previous result, |r| < m) instead of 0.
 hipError_t launch_combine_exact(const int64_t* in, uint64_t n, uint64_t dim, uint64_t stride,
-                                int64_t* out, int64_t modulus, hipStream_t s);
+                                int64_t* out, int64_t modulus, hipStream_t s, bool accumulate = false);
 // Canonical residue of u64 sums (multi-GPU finalize).
 hipError_t launch_mod_canonical(const int64_t* sums, uint64_t dim, int64_t* out, int64_t modulus,
                                 hipStream_t s);

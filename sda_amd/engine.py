@@ -77,6 +77,7 @@ SIGNATURES = [
     ("sda_recipient_positive", _st, [_vp, C.c_int64, _i64p, C.c_uint64, _i64p]),
     ("sda_combine_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp, _vp]),
     ("sda_combine_finalize_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, _vp, _vp]),
+    ("sda_combine_accumulate_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp, _vp]),
     ("sda_packed_generate_dev", _st, [_vp, C.POINTER(S.SharingSchemeC), _vp, C.c_uint64, C.c_uint64, _vp, _vp,
                                       _vp]),
     ("sda_packed_reconstruct_dev", _st, [_vp, C.POINTER(S.SharingSchemeC), C.c_uint64, _u64p, C.c_uint64,
@@ -293,6 +294,10 @@ class Engine:
     # ---------------- device-resident entry points (raw device pointers, hipStream_t) ----------------
     def combine_dev(self, modulus, shares_ptr, n, dim, row_stride, out_ptr, stream=None):
         _check(self.lib.sda_combine_dev(self.h, modulus, shares_ptr, n, dim, row_stride, out_ptr, stream))
+
+    def combine_accumulate_dev(self, modulus, shares_ptr, n, dim, row_stride, inout_ptr, stream=None):
+        _check(self.lib.sda_combine_accumulate_dev(self.h, modulus, shares_ptr, n, dim, row_stride, inout_ptr,
+                                                   stream))
 
     def combine_finalize_dev(self, modulus, sums_ptr, dim, out_ptr, stream=None):
         _check(self.lib.sda_combine_finalize_dev(self.h, modulus, sums_ptr, dim, out_ptr, stream))

@@ -146,3 +146,17 @@ def test_packed_generate_fixup_overflow(engine, oracle):
     for b in list(np.random.default_rng(3).integers(0, B, 48)) + [0, B - 1]:
         exp = oracle.packed_share(pp, padded[b * k:(b + 1) * k], draws[b])
         assert_same(shares[:, b], exp)
+
+
+def test_combine_accumulate_tiles(engine, oracle):
+    """sda_combine_accumulate_dev: a job streamed in row tiles == one pass (signed, order-dependent)."""
+    m = 2147482801
+    N, D = 37, 3001
+    x = np.random.default_rng(9).integers(-(m - 1), m, size=(N, D), dtype=np.int64)
+    xd = torch.as_tensor(x).cuda()
+    acc = torch.zeros(D, dtype=torch.int64, device="cuda")
+    for t0 in range(0, N, 10):
+        n = min(10, N - t0)
+        engine.combine_accumulate_dev(m, xd[t0].data_ptr(), n, D, D, acc.data_ptr())
+    torch.cuda.synchronize()
+    assert_same(acc.cpu().numpy(), oracle.combine(m, x))
