@@ -12,7 +12,7 @@
 // The clerk decrypts N participations (sodium stays on the host) and combines them
 // (clerk.rs:79-86).  On the device the blobs are one concatenated byte stream; decoding is a
 // stream compaction over terminator bytes (b & 0x80 == 0):
-//   pass A  per 4 KiB aligned region of a blob: count terminators, flag runs of >= 11
+//   pass A  per 16 KiB aligned region of a blob: count terminators, flag runs of >= 11
 //           continuation bytes ("irregular" blob);
 //   pass B  per blob: exclusive scan of its region counts -> element base per region, total;
 //   pass C  per region: each terminator byte decodes the <= 10-byte varint that ends at it (its
@@ -25,11 +25,12 @@ namespace sda {
 
 namespace {
 
-constexpr int kThreads = 256;                 // one 16-byte word per thread
-constexpr uint64_t kRegionBytes = kThreads * 16;
-#ifndef SDA_DECODE_STAGE_OUT
-#define SDA_DECODE_STAGE_OUT 0
-#endif
+constexpr int kThreads = 256;
+constexpr int kWPT = 4;                       // 16-byte words per thread: word t + 256 k, k < kWPT
+constexpr uint64_t kSubBytes = kThreads * 16; // one sub-region = one word per thread
+constexpr uint64_t kRegionBytes = kSubBytes * kWPT;
+
+
 
 // 16 bytes as a 16-bit mask of "continuation" bytes (bit j = byte j has 0x80).
 __device__ __forceinline__ uint32_t cont_mask(uint4 w) {
@@ -59,13 +60,11 @@ struct Window {
     uint32_t valid, term, cont;
 };
 
-__device__ __forceinline__ Window load_window(const uint8_t* __restrict__ base_aligned, uint64_t word, uint64_t begin,
-                                              uint64_t end) {
+__device__ __forceinline__ Window make_window(uint4 prev, uint4 own, uint64_t word, uint64_t begin, uint64_t end) {
     Window W;
     const uint64_t a0 = word * 16;                      // byte offset of own word (aligned)
-    const uint4* p = reinterpret_cast<const uint4*>(base_aligned);
-    W.own = (a0 < end) ? p[word] : make_uint4(0, 0, 0, 0);
-    W.prev = (a0 >= 16 && a0 - 16 < end && a0 > begin) ? p[word - 1] : make_uint4(0, 0, 0, 0);
+    W.own = own;
+    W.prev = prev;
     const uint32_t cm = cont_mask(W.prev) | (cont_mask(W.own) << 16);
     // window byte j sits at a0 - 16 + j
     uint32_t in = 0;
@@ -84,7 +83,7 @@ __device__ __forceinline__ Window load_window(const uint8_t* __restrict__ base_a
     return W;
 }
 
-// 2-D grid: blockIdx.y = blob (+ y0), blockIdx.x = region within the blob (4 KiB aligned to the
+// 2-D grid: blockIdx.y = blob (+ y0), blockIdx.x = region within the blob (16 KiB aligned to the
 // byte buffer).  Blocks past a blob's last region exit at once (payload blobs have near-equal sizes).
 __device__ __forceinline__ bool region_of(const uint64_t* __restrict__ blob_region,
                                           const uint64_t* __restrict__ blob_off, uint32_t y0, uint32_t* blob,
@@ -107,14 +106,41 @@ __global__ __launch_bounds__(kThreads) void varint_count_kernel(const uint8_t* _
     uint32_t b;
     uint64_t r, word;
     if (!region_of(blob_region, blob_off, y0, &b, &r, &word)) return;
-    word += threadIdx.x;
-    const Window W = load_window(bytes, word, blob_off[b], blob_off[b + 1]);
-    uint32_t n = __builtin_popcount(W.term & W.valid);
-    // 11 continuation bytes in a row ending inside this word?
-    uint32_t run = W.cont;
+    const uint64_t begin = blob_off[b], end = blob_off[b + 1];
+    // one coalesced load per word; the previous word's continuation mask (for the run check across
+    // the word boundary) comes through LDS
+    __shared__ uint32_t cm_l[kWPT * kThreads + 1];
+    const uint4* p = reinterpret_cast<const uint4*>(bytes);
+    uint4 v[kWPT];
 #pragma unroll
-    for (int k = 1; k <= 10; ++k) run &= W.cont << k;
-    if (run & W.valid) atomicOr(&blob_irregular[b], 1u);
+    for (int k = 0; k < kWPT; ++k) {
+        const uint64_t wk = word + threadIdx.x + k * kThreads;
+        v[k] = wk * 16 < end ? p[wk] : make_uint4(0, 0, 0, 0);
+    }
+    uint4 halo = make_uint4(0, 0, 0, 0);
+    if (threadIdx.x == 0 && word * 16 > begin) halo = p[word - 1];
+    Window W[kWPT];
+#pragma unroll
+    for (int k = 0; k < kWPT; ++k) {
+        const uint32_t wl = threadIdx.x + k * kThreads;
+        W[k] = make_window(make_uint4(0, 0, 0, 0), v[k], word + wl, begin, end);   // own-word masks only
+        cm_l[wl + 1] = W[k].cont >> 16;
+    }
+    if (threadIdx.x == 0) cm_l[0] = make_window(make_uint4(0, 0, 0, 0), halo, word - 1, begin, end).cont >> 16;
+    __syncthreads();
+    uint32_t n = 0, bad = 0;
+#pragma unroll
+    for (int k = 0; k < kWPT; ++k) {
+        const uint32_t wl = threadIdx.x + k * kThreads;
+        n += __builtin_popcount(W[k].term & W[k].valid);
+        // 11 continuation bytes in a row ending inside this word?
+        const uint32_t cont = W[k].cont | cm_l[wl];
+        uint32_t run = cont;
+#pragma unroll
+        for (int q = 1; q <= 10; ++q) run &= cont << q;
+        bad |= run & W[k].valid;
+    }
+    if (bad) atomicOr(&blob_irregular[b], 1u);
     // block reduction (one value per region)
     __shared__ uint32_t red[kThreads / 64];
     for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
@@ -165,11 +191,11 @@ __device__ __forceinline__ uint64_t leb_pack8(uint64_t x) {
     return x;
 }
 
-// pass C: decode.  The region's bytes (plus a 16-byte halo on each side) are staged in LDS; each
-// terminator byte decodes the varint ending at it from three funnel-shifted dwords; the values are
-// parked in LDS by element index and written back with coalesced stores.  Element index of a
-// terminator = region base + terminators before it in the region.  Blobs flagged irregular are
-// skipped here (varint_sequential_kernel).
+// pass C: decode.  The region's bytes (plus a 16-byte halo on each side) are staged in LDS; the
+// region is walked as kWPT sub-regions of one word per thread.  Per sub-region a block-wide scan
+// of the terminator counts compacts the elements' (start, length) into LDS; then lane i decodes
+// element i (balanced work, coalesced stores) from three funnel-shifted dwords.  Element index of a terminator = region base + terminators before it in
+// the region.  Blobs flagged irregular are skipped here (varint_sequential_kernel).
 __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* __restrict__ bytes,
                                                                  const uint64_t* __restrict__ blob_region,
                                                                  const uint64_t* __restrict__ blob_off, uint32_t y0,
@@ -179,66 +205,85 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
     uint32_t b;
     uint64_t r, word;
     if (!region_of(blob_region, blob_off, y0, &b, &r, &word) || blob_irregular[b]) return;
-    __shared__ uint32_t lb[(kRegionBytes + 32) / 4];          // [halo 16 B | region 4 KiB | tail 16 B]
-#if SDA_DECODE_STAGE_OUT
-    __shared__ int64_t lv[kRegionBytes];                      // decoded values by region-local index
-#endif
+    __shared__ uint32_t lb[(kRegionBytes + 32) / 4];          // [halo 16 B | region 16 KiB | tail 16 B]
     __shared__ uint32_t wsum[kThreads / 64];
-    word += threadIdx.x;
-    const Window W = load_window(bytes, word, blob_off[b], blob_off[b + 1]);
-    reinterpret_cast<uint4*>(lb)[threadIdx.x + 1] = W.own;
-    if (threadIdx.x == 0) reinterpret_cast<uint4*>(lb)[0] = W.prev;
-    if (threadIdx.x == kThreads - 1) reinterpret_cast<uint4*>(lb)[kThreads + 1] = make_uint4(0, 0, 0, 0);
-    const uint32_t tm = W.term & W.valid;
-    const uint32_t n = __builtin_popcount(tm);
-    uint32_t incl = n;                                        // exclusive scan of n over the block
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o);
-        if ((threadIdx.x & 63) >= (uint32_t)o) incl += t;
-    }
-    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
-    __syncthreads();
-    uint32_t e = incl - n;
-    uint32_t total = 0;
-    for (uint32_t w = 0; w < kThreads / 64; ++w) {
-        if (w < (threadIdx.x >> 6)) e += wsum[w];
-        total += wsum[w];
-    }
-    // the element ending at window position j starts after the previous boundary (a terminator or
-    // a byte outside the blob)
-    const uint32_t boundary = W.term | ~(W.term | W.cont);
-    int64_t* dst = out + (uint64_t)b * out_stride + region_base[r];
-    (void)total;
-    uint32_t rem = tm;
-    while (rem) {
-        const int j = __builtin_ctz(rem);
-        rem &= rem - 1;
-        const uint32_t below = boundary & ((1u << j) - 1u);
-        const int st = below ? 32 - __builtin_clz(below) : 0;      // window index of the first byte
-        const int len = j - st + 1;                                 // 1..11 on regular blobs
-        const uint32_t P = threadIdx.x * 16 + st;                   // byte position in lb
-        const uint32_t q = P >> 2, sh = (P & 3) * 8;
-        const uint32_t d0 = lb[q], d1 = lb[q + 1], d2 = lb[q + 2], d3 = lb[q + 3];
-        const uint32_t b0 = __builtin_amdgcn_alignbit(d1, d0, sh), b1 = __builtin_amdgcn_alignbit(d2, d1, sh),
-                       b2 = __builtin_amdgcn_alignbit(d3, d2, sh);
-        uint64_t lo = ((uint64_t)b1 << 32) | b0;
-        if (len < 8) lo &= (1ull << (8 * len)) - 1;
-        uint64_t z = leb_pack8(lo);
-        if (len > 8) {                  // groups 8, 9, 10 at shifts 56, 63, 70 & 63 = 6 (Rust release)
-            const uint32_t hb = b2 & ((len >= 11) ? 0xFFFFFFu : (len == 10 ? 0xFFFFu : 0xFFu));
-            z |= ((uint64_t)(hb & 0x7F) << 56) | ((uint64_t)((hb >> 8) & 0x7F) << 63) |
-                 ((uint64_t)((hb >> 16) & 0x7F) << 6);
+    __shared__ uint32_t el[kSubBytes];                        // one sub-region's elements: start | len << 16
+    const uint64_t begin = blob_off[b], end = blob_off[b + 1];
+    // stage the region's words (one coalesced load each) and the halo word before it; the windows
+    // (previous word + own word) are then read back from LDS
+    {
+        const uint4* p = reinterpret_cast<const uint4*>(bytes);
+        uint4 v[kWPT];
+#pragma unroll
+        for (int k = 0; k < kWPT; ++k) {
+            const uint64_t wk = word + threadIdx.x + k * kThreads;
+            v[k] = wk * 16 < end ? p[wk] : make_uint4(0, 0, 0, 0);
         }
-#if SDA_DECODE_STAGE_OUT
-        lv[e++] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
-#else
-        dst[e++] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
-#endif
+        if (threadIdx.x == 0)
+            reinterpret_cast<uint4*>(lb)[0] = (word * 16 > begin) ? p[word - 1] : make_uint4(0, 0, 0, 0);
+        if (threadIdx.x == kThreads - 1) reinterpret_cast<uint4*>(lb)[kWPT * kThreads + 1] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < kWPT; ++k) reinterpret_cast<uint4*>(lb)[threadIdx.x + k * kThreads + 1] = v[k];
     }
-#if SDA_DECODE_STAGE_OUT
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < total; i += kThreads) dst[i] = lv[i];
-#endif
+    Window W[kWPT];
+#pragma unroll
+    for (int k = 0; k < kWPT; ++k) {
+        const uint32_t wl = threadIdx.x + k * kThreads;
+        W[k] = make_window(reinterpret_cast<const uint4*>(lb)[wl], reinterpret_cast<const uint4*>(lb)[wl + 1],
+                           word + wl, begin, end);
+    }
+    int64_t* dst = out + (uint64_t)b * out_stride + region_base[r];
+    uint32_t base = 0;                                        // elements in earlier sub-regions
+#pragma unroll
+    for (int k = 0; k < kWPT; ++k) {
+        // 1. compaction: each thread lists the (start, length) of the elements ending in its word
+        const uint32_t tm = W[k].term & W[k].valid;
+        const uint32_t n = __builtin_popcount(tm);
+        uint32_t incl = n;                                    // exclusive scan of n over the block
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o);
+            if ((threadIdx.x & 63) >= (uint32_t)o) incl += t;
+        }
+        __syncthreads();                                      // lb visible; el / wsum free for reuse
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        uint32_t e = incl - n, total = 0;
+        for (uint32_t w = 0; w < kThreads / 64; ++w) {
+            if (w < (threadIdx.x >> 6)) e += wsum[w];
+            total += wsum[w];
+        }
+        // an element starts after the previous boundary (a terminator or a byte outside the blob)
+        const uint32_t boundary = W[k].term | ~(W[k].term | W[k].cont);
+        uint32_t rem = tm;
+        while (rem) {
+            const int j = __builtin_ctz(rem);
+            rem &= rem - 1;
+            const uint32_t below = boundary & ((1u << j) - 1u);
+            const int st = below ? 32 - __builtin_clz(below) : 0;      // window index of the first byte
+            el[e++] = ((threadIdx.x + k * kThreads) * 16 + st) | ((uint32_t)(j - st + 1) << 16);
+        }
+        __syncthreads();
+        // 2. decode: lane i takes element i -> balanced work, coalesced stores
+        for (uint32_t i = threadIdx.x; i < total; i += kThreads) {
+            const uint32_t P = el[i] & 0xFFFFu;                  // byte position in lb
+            const int len = (int)(el[i] >> 16);                   // 1..11 on regular blobs
+            const uint32_t q = P >> 2, sh = (P & 3) * 8;
+            const uint32_t d0 = lb[q], d1 = lb[q + 1], d2 = lb[q + 2], d3 = lb[q + 3];
+            const uint32_t b0 = __builtin_amdgcn_alignbit(d1, d0, sh), b1 = __builtin_amdgcn_alignbit(d2, d1, sh),
+                           b2 = __builtin_amdgcn_alignbit(d3, d2, sh);
+            uint64_t lo = ((uint64_t)b1 << 32) | b0;
+            if (len < 8) lo &= (1ull << (8 * len)) - 1;
+            uint64_t z = leb_pack8(lo);
+            if (len > 8) {              // groups 8, 9, 10 at shifts 56, 63, 70 & 63 = 6 (Rust release)
+                const uint32_t hb = b2 & ((len >= 11) ? 0xFFFFFFu : (len == 10 ? 0xFFFFu : 0xFFu));
+                z |= ((uint64_t)(hb & 0x7F) << 56) | ((uint64_t)((hb >> 8) & 0x7F) << 63) |
+                     ((uint64_t)((hb >> 16) & 0x7F) << 6);
+            }
+            dst[base + i] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
+        }
+        base += total;
+    }
 }
 
 // Irregular blobs: the reference loop, one lane per blob (only malformed streams get here).
