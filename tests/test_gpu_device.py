@@ -160,3 +160,22 @@ def test_combine_accumulate_tiles(engine, oracle):
         engine.combine_accumulate_dev(m, xd[t0].data_ptr(), n, D, D, acc.data_ptr())
     torch.cuda.synchronize()
     assert_same(acc.cpu().numpy(), oracle.combine(m, x))
+
+
+def test_distributed_helpers_single_rank(engine, oracle):
+    """sda_amd.distributed's device paths at world size 1 (the multi-rank reduce is covered with
+    gloo in test_host.py): seed-split ChaCha mask combine and the column-split signed combine."""
+    from sda_amd import distributed as Dd
+    m, D = 2147482801, 5001
+    seeds = torch.randint(0, 2**31 - 1, (7, 4), dtype=torch.int32, device="cuda",
+                          generator=torch.Generator(device="cuda").manual_seed(3))
+    part = torch.empty(D, dtype=torch.int64, device="cuda")
+    out = torch.empty(D, dtype=torch.int64, device="cuda")
+    Dd.mask_combine_sharded(engine, m, D, seeds, part, out)
+    torch.cuda.synchronize()
+    assert_same(out.cpu().numpy(), oracle.chacha_mask_combine(m, D, seeds.cpu().numpy().astype(np.int64)))
+    x = np.random.default_rng(12).integers(-(m - 1), m, size=(19, D), dtype=np.int64)
+    xd = torch.as_tensor(x).cuda()
+    Dd.combine_columns_sharded(engine, m, xd, out)
+    torch.cuda.synchronize()
+    assert_same(out.cpu().numpy(), oracle.combine(m, x))

@@ -75,3 +75,53 @@ def test_gloo_world2_sharded_combine_matches_single_pass():
     for p in procs:
         p.join(timeout=60)
     assert got == exp
+
+
+def _worker2(rank, world, port, q):
+    """reduce_canonical over the ChaCha mask N-split, and the column split of a signed combine,
+    with the oracle as the per-rank compute stand-in."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    m, D = 2147482801, 301
+    seeds = (np.arange(10 * 4, dtype=np.int64).reshape(10, 4) * 7919) % (1 << 31)
+    s0, c = Dd.shard_range(10, rank, world)
+    part = torch.from_numpy(O.chacha_mask_combine(m, D, seeds[s0:s0 + c]))
+    out = torch.empty(D, dtype=torch.int64)
+    Dd.reduce_canonical(part, m, lambda p, o: o.copy_(torch.remainder(p, m)), out)
+    res = {"mask": (out.tolist(), O.chacha_mask_combine(m, D, seeds).tolist())}
+    x = synth.fill(23, D, 0x5DA + 9, -(m - 1), m)         # signed: order-dependent exact result
+    lo, cnt = Dd.column_slice(D, rank, world)
+    width = max(Dd.column_slice(D, r, world)[1] for r in range(world))
+    mine = torch.zeros(width, dtype=torch.int64)
+    mine[:cnt] = torch.from_numpy(O.combine(m, np.ascontiguousarray(x[:, lo:lo + cnt])))
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine)
+    full = torch.cat([parts[r][:Dd.column_slice(D, r, world)[1]] for r in range(world)])
+    res["columns"] = (full.tolist(), O.combine(m, x).tolist())
+    if rank == 0:
+        q.put(res)
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_mask_reduce_and_column_split():
+    """sda_amd.distributed: ChaCha mask combine split over seeds + reduce_canonical, and the signed
+    combine split over columns + all-gather, equal the single-pass reference (gloo, world 2)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker2, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    for k, (got, exp) in res.items():
+        assert got == exp, k
+
+
+@pytest.mark.parametrize("dim,world", [(1, 2), (7, 3), (1000, 8), (5, 8)])
+def test_column_slice_partitions(dim, world):
+    sl = [Dd.column_slice(dim, r, world) for r in range(world)]
+    cols = [c for lo, n in sl for c in range(lo, lo + n)]
+    assert cols == list(range(dim)) and all(lo % 2 == 0 for lo, n in sl if n)
