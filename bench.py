@@ -209,7 +209,22 @@ def main():
         idx = list(range(n - (t + k), n))           # a t+k clerk subset (result_ready threshold)
         sub = torch.empty((V, len(idx), B), dtype=torch.int64, device=dev)
         rev = torch.empty((V, Dm), dtype=torch.int64, device=dev)
-        gen_t, rex_t, rca_t = Timer(torch), Timer(torch), Timer(torch)
+        gen_t, rex_t, rca_t, gca_t = Timer(torch), Timer(torch), Timer(torch), Timer(torch)
+        # canonical-mode share-gen first (its shares are overwritten by the exact ones below)
+        genc = lambda: eng.packed_generate_mode_dev(sch, sec.data_ptr(), Dm, V, drw.data_ptr(), sh.data_ptr(),  # noqa
+                                                    E.REVEAL_CANONICAL, stream())
+        for i in range(args.warmup + args.steps):
+            gca_t.record(genc) if i >= args.warmup else genc()
+        torch.cuda.synchronize()
+        if not args.no_check:     # canonical shares: in [0, p) and a canonical reveal returns the secrets
+            sub0 = sh[:, n - (t + k):, :].contiguous()
+            rv = torch.empty((V, Dm), dtype=torch.int64, device=dev)
+            eng.packed_reconstruct_dev(sch, Dm, list(range(n - (t + k), n)), V, sub0.data_ptr(), rv.data_ptr(),
+                                       E.REVEAL_CANONICAL, stream())
+            torch.cuda.synchronize()
+            if int(sh.min()) < 0 or not torch.equal(rv, sec):
+                raise SystemExit("canonical share-gen round trip FAILED")
+            del sub0, rv
         gen = lambda: eng.packed_generate_dev(sch, sec.data_ptr(), Dm, V, drw.data_ptr(), sh.data_ptr(), stream())  # noqa
         for i in range(args.warmup + args.steps):
             gen_t.record(gen) if i >= args.warmup else gen()
@@ -221,7 +236,7 @@ def main():
             torch.cuda.synchronize()
             if not args.no_check and not torch.equal(torch.remainder(rev, p), sec):
                 raise SystemExit(f"packed reveal round-trip FAILED (mode {mode})")
-        g_ms, x_ms, c_ms = gen_t.mean_ms(), rex_t.mean_ms(), rca_t.mean_ms()
+        g_ms, x_ms, c_ms, gc_ms = gen_t.mean_ms(), rex_t.mean_ms(), rca_t.mean_ms(), gca_t.mean_ms()
         gen_bytes = 8.0 * V * (Dm + t * B + n * B)
         rev_bytes = 8.0 * V * (len(idx) * B + Dm)
         side["shamir"] = {
@@ -229,6 +244,8 @@ def main():
             "shares_per_s": V * n * B / (g_ms * 1e-3),
             "gen_ms": g_ms, "gen_GBps": gen_bytes / (g_ms * 1e-3) / 1e9,
             "gen_roofline_frac": gen_bytes / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "gen_canonical_ms": gc_ms, "gen_canonical_GBps": gen_bytes / (gc_ms * 1e-3) / 1e9,
+            "gen_canonical_roofline_frac": gen_bytes / (gc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
             "reveal_exact_ms": x_ms, "reveal_exact_GBps": rev_bytes / (x_ms * 1e-3) / 1e9,
             "reveal_canonical_ms": c_ms, "reveal_canonical_GBps": rev_bytes / (c_ms * 1e-3) / 1e9,
             "reveal_clerks": len(idx),

@@ -176,6 +176,14 @@ sda_status sda_packed_generate_dev(sda_engine* h, const sda_sharing_scheme* s,
                                    const int64_t* secrets, uint64_t dimension, uint64_t n_vectors,
                                    const int64_t* draws, int64_t* out, void* stream);
 
+/* The same with a representation mode: SDA_REVEAL_EXACT = tss' signed shares (as above),
+ * SDA_REVEAL_CANONICAL = their canonical residues in [0, p).  Canonical shares are equal to the
+ * reference's mod p, so combine -> reveal -> unmask -> positive() ends in the identical output
+ * when the masking modulus is the sharing prime. */
+sda_status sda_packed_generate_mode_dev(sda_engine* h, const sda_sharing_scheme* s,
+                                        const int64_t* secrets, uint64_t dimension, uint64_t n_vectors,
+                                        const int64_t* draws, int64_t* out, int32_t mode, void* stream);
+
 /* Packed-Shamir reveal: shares [n_vectors][n_idx][B] at clerk `indices` (host array),
  * out [n_vectors][dimension]. */
 sda_status sda_packed_reconstruct_dev(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,

@@ -562,6 +562,22 @@ sda_status sda_packed_generate_dev(sda_engine* h, const sda_sharing_scheme* s, c
     return ok();
 }
 
+sda_status sda_packed_generate_mode_dev(sda_engine* h, const sda_sharing_scheme* s, const int64_t* secrets,
+                                        uint64_t dimension, uint64_t n_vectors, const int64_t* draws, int64_t* out,
+                                        int32_t mode, void* stream) {
+    if (!h || !s || s->kind != SDA_SHARING_PACKED_SHAMIR) return fail(SDA_ERR_INVALID_ARGUMENT, "need a PackedShamir scheme");
+    if (mode != SDA_REVEAL_EXACT && mode != SDA_REVEAL_CANONICAL) return fail(SDA_ERR_INVALID_ARGUMENT, "bad mode");
+    if (sda_status st = check_packed(s)) return st;
+    if (n_vectors > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 vectors per launch");
+    HIP_TRY(hipSetDevice(h->device));
+    sda::PackedGenArgs ga{secrets, dimension, n_vectors, draws, out, mode == SDA_REVEAL_CANONICAL};
+    if (sda_status st = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return st;
+    HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)s->secret_count, (uint32_t)s->privacy_threshold,
+                                        (uint32_t)s->share_count, (uint32_t)s->modulus, (uint32_t)s->omega_secrets,
+                                        (uint32_t)s->omega_shares, h->gen_tab, h->gen_log, pick(h, stream)));
+    return ok();
+}
+
 sda_status sda_packed_reconstruct_dev(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,
                                       const uint64_t* indices, uint64_t n_idx, uint64_t n_vectors,
                                       const int64_t* shares, int64_t* out, int32_t mode, void* stream) {

@@ -47,6 +47,7 @@ void free_table(DeviceTable& t);
 struct PackedGenArgs {
     const int64_t* secrets; uint64_t dimension; uint64_t n_vectors;
     const int64_t* draws; int64_t* out;
+    bool canonical = false;       // shares as canonical residues in [0, p) instead of tss' signed values
 };
 // Batches whose inputs fall outside (-p, p) are logged by the fast kernel and recomputed by a
 // generic exact fix-up kernel.  `log_buf` is device memory of packed_gen_log_bytes() bytes.

@@ -61,6 +61,71 @@ constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
 #endif
 
 
+// CANONICAL share generation: the same transform in canonical residues [0, p) only -- no sign
+// tracking.  Each share equals tss' (signed) share mod p, so everything downstream (combine,
+// reveal, unmask, RecipientOutput::positive) ends in the same canonical output when the masking
+// modulus is the sharing prime.  Radix-3 groups use omega_3 = omega_len^(len/3):
+// with C = x c, D = x^2 d:  y0 = b + C + D,  y1 = b - D + w3 (C - D),  y2 = b - C - w3 (C - D)
+// -- 3 Montgomery products per 3 outputs instead of 6.
+template <int L, int N3>
+__device__ __forceinline__ void transform_canon(const int64_t (&raw)[L], const GenTables& T, const MontP& M,
+                                                int32_t (&ys)[N3]) {
+    constexpr int LB = ilog(L, 2);
+    constexpr int ND = ilog(N3, 3);
+    using Z = Zero3<L, N3>;
+    const uint32_t p = M.p;
+    auto mont = [&](uint32_t a_m, uint32_t x) { return red1(redc_lazy((uint64_t)a_m * x, M), p); };
+    uint32_t x[L];
+    static_for<0, L>([&](auto i) { x[rev_digits(i, 2, LB)] = canon32((int32_t)raw[i], p); });
+    static_for<1, LB + 1>([&](auto s) {
+        constexpr int H = 1 << (s - 1), LEN = 2 * H;
+        static_for<0, L, LEN>([&](auto g) {
+            static_for<0, H>([&](auto i) {
+                const uint32_t u = x[g + i];
+                const uint32_t c = (i == 0) ? x[g + i + H] : mont(T.tw2_m[H - 1 + i], x[g + i + H]);
+                x[g + i] = addm(u, c, p);
+                x[g + i + H] = subm(u, c, p);
+            });
+        });
+    });
+    static_for<0, L>([&](auto i) { x[i] = mont(T.linv_m, x[i]); });
+    uint32_t y[N3];
+    static_for<0, N3>([&](auto i) {
+        if constexpr (i < L) y[rev_digits(i, 3, ND)] = x[i < L ? (int)i : 0];
+        else y[rev_digits(i, 3, ND)] = 0u;
+    });
+    const uint32_t w3 = T.tw3_m[1];                      // omega_3 (stage len 3, j = 1), Montgomery form
+    static_for<1, ND + 1>([&](auto s) {
+        constexpr int th = ipow(3, s - 1);
+        constexpr int LEN = 3 * th, OB = (LEN - 3) / 2;
+        static_for<0, N3, LEN>([&](auto g) {
+            static_for<0, th>([&](auto i) {
+                constexpr bool zc = Z::is_zero(s - 1, g + i + th), zd = Z::is_zero(s - 1, g + i + 2 * th);
+                if constexpr (zc && zd) {
+                    y[g + i + th] = y[g + i];
+                    y[g + i + 2 * th] = y[g + i];
+                } else {
+                    const uint32_t bb = y[g + i];
+                    const uint32_t C = (i == 0) ? y[g + i + th] : mont(T.tw3_m[OB + i], y[g + i + th]);
+                    if constexpr (zd) {
+                        const uint32_t E = mont(w3, C);
+                        y[g + i] = addm(bb, C, p);
+                        y[g + i + th] = addm(bb, E, p);
+                        y[g + i + 2 * th] = subm(subm(bb, C, p), E, p);
+                    } else {
+                        const uint32_t Dd = (i == 0) ? y[g + i + 2 * th] : mont(T.sq3_m[OB + i], y[g + i + 2 * th]);
+                        const uint32_t E = mont(w3, subm(C, Dd, p));
+                        y[g + i] = addm(addm(bb, C, p), Dd, p);
+                        y[g + i + th] = addm(subm(bb, Dd, p), E, p);
+                        y[g + i + 2 * th] = subm(subm(bb, C, p), E, p);
+                    }
+                }
+            });
+        });
+    });
+    static_for<0, N3>([&](auto j) { ys[j] = (int32_t)y[j]; });
+}
+
 // One workgroup = one tile (vector blockIdx.y, BS batches from blockIdx.x * BS).
 //
 // Lane -> batch map: lane i < 32 takes batch 2i of its wave's 64, lane 32 + i batch 2i + 1.  After
@@ -69,7 +134,7 @@ constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
 // per row pair (13 dwordx4 instead of 26 dwordx2 at n = 26) when WIDE (B even, 16-B aligned out).
 // (A persistent grid-stride variant was measured slower: the loop made hipcc keep the twiddle
 // words in SGPRs across tiles and spill.)
-template <int L, int N3, bool WIDE>
+template <int L, int N3, bool WIDE, bool CANON>
 __global__ __launch_bounds__(gen_block<L>()) __attribute__((amdgpu_waves_per_eu(SDA_GEN_WAVES)))
 void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const int64_t* __restrict__ draws,
                        int64_t* __restrict__ out, uint32_t k, uint32_t t, uint64_t B,
@@ -111,7 +176,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                 int64_t v[U];
                 static_for<0, U>([&](auto u) {
                     const uint32_t e = base + u * BS + tid;
-                    v[u] = ssrc[e < valid ? e : 0];
+                    v[u] = __builtin_nontemporal_load(ssrc + (e < valid ? e : 0));   // read once
                 });
                 static_for<0, U>([&](auto u) {
                     const uint32_t e = base + u * BS + tid;
@@ -125,7 +190,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                 int64_t v[U];
                 static_for<0, U>([&](auto u) {
                     const uint32_t e = base + u * BS + tid;
-                    v[u] = dsrc[e < nd ? e : 0];
+                    v[u] = __builtin_nontemporal_load(dsrc + (e < nd ? e : 0));
                 });
                 static_for<0, U>([&](auto u) {
                     const uint32_t e = base + u * BS + tid;
@@ -159,6 +224,10 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
             if (slot < kGenLogCap) reinterpret_cast<uint64_t*>(log + 16)[slot] = (uint64_t)vec * B + b;
         }
 
+        int32_t ys[N3];                  // shares (tss' signed values, or canonical residues)
+        if constexpr (CANON) {
+            transform_canon<L, N3>(raw, T, M, ys);
+        } else {
         // ---- fft2_inverse: radix-2 DIT over omega_secrets^-1 on bit-reversed registers ----
         FE x[L];
         static_for<0, L>([&](auto i) {
@@ -239,13 +308,16 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
             });
         });
 
+        static_for<0, N3>([&](auto j) { ys[j] = y[j].s; });
+        }
+
         // ---- shares = points[1..=n], clerk-major (batched.rs:46-48) ----
         const uint64_t pb = b0 + pb_off;
         const bool st1 = pair_ok && pb + 1 < B;
         int64_t* orow = out + ((uint64_t)vec * NR + half) * B + pb;
         if constexpr (WIDE) {              // B even => pb + 1 < B whenever pb < B
             static_for<0, NR / 2>([&](auto q) {
-                const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)y[1 + 2 * q].s, (uint32_t)y[2 + 2 * q].s,
+                const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)ys[1 + 2 * q], (uint32_t)ys[2 + 2 * q],
                                                                 false, false);
                 const int32_t lo = (int32_t)r[0], hi = (int32_t)r[1];  // batches pb, pb + 1 of row 1+2q+half
                 if (st1) {
@@ -257,26 +329,33 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
             });
         } else {                           // odd B: each lane stores its own batch
             int64_t* own = out + (uint64_t)vec * NR * B + b;
-            static_for<1, N3>([&](auto j) { if (live && pair_ok) own[(uint64_t)(j - 1) * B] = (int64_t)y[j].s; });
+            static_for<1, N3>([&](auto j) { if (live && pair_ok) own[(uint64_t)(j - 1) * B] = (int64_t)ys[j]; });
         }
     }
 }
 
 }  // namespace
 
+template <int L, int N3, bool CANON>
+static void gen_launch_mode(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
+                            const GenFixupLog& log, hipStream_t s) {
+    constexpr int BS = gen_block<L>();
+    const dim3 grid((unsigned)((B + BS - 1) / BS), (unsigned)a.n_vectors);
+    if (B % 2 == 0 && ((uintptr_t)a.out % 16) == 0)
+        hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, CANON>), grid, dim3(BS), 0, s, a.secrets, a.dimension,
+                           a.draws, a.out, k, t, B, T, log.count);
+    else
+        hipLaunchKernelGGL((packed_gen_kernel<L, N3, false, CANON>), grid, dim3(BS), 0, s, a.secrets, a.dimension,
+                           a.draws, a.out, k, t, B, T, log.count);
+}
+
 template <int L, int N3>
 static hipError_t gen_launch(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
                              const GenFixupLog& log, hipStream_t s) {
     constexpr int BS = gen_block<L>();
-    const uint64_t tiles_x = (B + BS - 1) / BS;
-    if (tiles_x > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)tiles_x, (unsigned)a.n_vectors);
-    if (B % 2 == 0 && ((uintptr_t)a.out % 16) == 0)
-        hipLaunchKernelGGL((packed_gen_kernel<L, N3, true>), grid, dim3(BS), 0, s, a.secrets, a.dimension, a.draws,
-                           a.out, k, t, B, T, log.count);
-    else
-        hipLaunchKernelGGL((packed_gen_kernel<L, N3, false>), grid, dim3(BS), 0, s, a.secrets, a.dimension, a.draws,
-                           a.out, k, t, B, T, log.count);
+    if ((B + BS - 1) / BS > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    if (a.canonical) gen_launch_mode<L, N3, true>(a, k, t, B, T, log, s);
+    else gen_launch_mode<L, N3, false>(a, k, t, B, T, log, s);
     return hipGetLastError();
 }
 
@@ -355,7 +434,8 @@ __global__ __launch_bounds__(256) void packed_gen_fixup_kernel(const int64_t* __
                                                                const int64_t* __restrict__ draws,
                                                                int64_t* __restrict__ out, uint32_t k, uint32_t t,
                                                                uint64_t B, uint64_t n_vec, int L, int N3,
-                                                               const GenTables* __restrict__ T, GenFixupLog log) {
+                                                               const GenTables* __restrict__ T, GenFixupLog log,
+                                                               int canonical) {
     const uint32_t n = *log.count;
     if (n == 0) return;
     const bool all = n > log.cap;
@@ -363,8 +443,13 @@ __global__ __launch_bounds__(256) void packed_gen_fixup_kernel(const int64_t* __
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t gb = all ? i : log.list[i];
         const uint64_t vec = gb / B, b = gb - vec * B;
-        packed_share_generic(secrets + vec * D, D, draws + gb * t, b, k, L, N3, *T,
-                             out + vec * (uint64_t)(N3 - 1) * B + b, B);
+        int64_t* o = out + vec * (uint64_t)(N3 - 1) * B + b;
+        packed_share_generic(secrets + vec * D, D, draws + gb * t, b, k, L, N3, *T, o, B);
+        if (canonical)                      // the exact share's canonical residue
+            for (int j = 1; j < N3; ++j) {
+                const int64_t v = o[(uint64_t)(j - 1) * B];
+                o[(uint64_t)(j - 1) * B] = v < 0 ? v + (int64_t)T->M.p : v;
+            }
     }
 }
 
@@ -399,7 +484,7 @@ hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t
     }
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(packed_gen_fixup_kernel, dim3(256), dim3(256), 0, s, a.secrets, a.dimension, a.draws, a.out,
-                       k, t, B, a.n_vectors, (int)L, (int)N3, T, log);
+                       k, t, B, a.n_vectors, (int)L, (int)N3, T, log, a.canonical ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -80,6 +80,8 @@ SIGNATURES = [
     ("sda_combine_accumulate_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp, _vp]),
     ("sda_packed_generate_dev", _st, [_vp, C.POINTER(S.SharingSchemeC), _vp, C.c_uint64, C.c_uint64, _vp, _vp,
                                       _vp]),
+    ("sda_packed_generate_mode_dev", _st, [_vp, C.POINTER(S.SharingSchemeC), _vp, C.c_uint64, C.c_uint64, _vp,
+                                           _vp, C.c_int32, _vp]),
     ("sda_packed_reconstruct_dev", _st, [_vp, C.POINTER(S.SharingSchemeC), C.c_uint64, _u64p, C.c_uint64,
                                          C.c_uint64, _vp, _vp, C.c_int32, _vp]),
     ("sda_additive_generate_dev", _st, [_vp, C.c_int64, C.c_uint64, _vp, C.c_uint64, _vp, _vp, _vp]),
@@ -306,6 +308,12 @@ class Engine:
         s = scheme.c()
         _check(self.lib.sda_packed_generate_dev(self.h, C.byref(s), secrets_ptr, dimension, n_vectors, draws_ptr,
                                                 out_ptr, stream))
+
+    def packed_generate_mode_dev(self, scheme, secrets_ptr, dimension, n_vectors, draws_ptr, out_ptr, mode,
+                                 stream=None):
+        s = scheme.c()
+        _check(self.lib.sda_packed_generate_mode_dev(self.h, C.byref(s), secrets_ptr, dimension, n_vectors,
+                                                     draws_ptr, out_ptr, mode, stream))
 
     def packed_reconstruct_dev(self, scheme, dimension, indices, n_vectors, shares_ptr, out_ptr,
                                mode=REVEAL_EXACT, stream=None):

@@ -306,3 +306,29 @@ def test_full_mask_unmask_positive(engine, oracle, m):
     assert_same(engine.secret_unmask(S.NoMasking(), ([], secrets)), secrets)
     with pytest.raises(SdaError):
         engine.secret_unmask(S.FullMasking(m), (masks[:-1], masked))
+
+
+@pytest.mark.parametrize("sch", packed_schemes(), ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")
+def test_packed_generate_canonical_mode(engine, oracle, sch):
+    """SDA_REVEAL_CANONICAL share-gen == the oracle's tss shares mod p (incl. raw i64 secrets)."""
+    import torch
+    p = sch.prime_modulus
+    rng = np.random.default_rng(p % 991 + sch.share_count)
+    D = 41 * sch.secret_count + 3
+    B = (D + sch.secret_count - 1) // sch.secret_count
+    secrets = rng.integers(-(p - 1), p, size=D, dtype=np.int64)
+    secrets[::7] = rng.integers(-(2**40), 2**40, size=secrets[::7].size, dtype=np.int64)
+    draws = rng.integers(0, p - 1, size=B * sch.privacy_threshold(), dtype=np.int64)
+    exp = np.mod(oracle.packed_generate(_pp(oracle, sch), secrets, draws), p)
+    for extra in (0, 1):                          # odd and even B (narrow and paired-wide stores)
+        s_ = np.concatenate([secrets, np.zeros(extra * sch.secret_count, np.int64)])
+        d_ = np.concatenate([draws, np.zeros(extra * sch.privacy_threshold(), np.int64)])
+        Bx = B + extra
+        ds, dd = torch.as_tensor(s_).cuda(), torch.as_tensor(d_).cuda()
+        out = torch.empty((sch.share_count, Bx), dtype=torch.int64, device="cuda")
+        engine.packed_generate_mode_dev(sch, ds.data_ptr(), s_.size, 1, dd.data_ptr(), out.data_ptr(),
+                                        E.REVEAL_CANONICAL)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert_same(got[:, :B], exp)
+        assert got.min() >= 0
