@@ -319,7 +319,8 @@ __device__ __forceinline__ uint32_t varint_size(int64_t v) {
     return (uint32_t)((bits + 6) / 7);
 }
 
-constexpr uint32_t kEncChunk = 4096;          // elements per encode block
+constexpr uint32_t kEncChunk = 2048;          // elements per encode block
+constexpr uint32_t kEncPer = kEncChunk / kThreads;
 
 // sizes of each [row][chunk] block of elements
 __global__ __launch_bounds__(kThreads) void varint_size_kernel(const int64_t* __restrict__ vals, uint64_t len,
@@ -328,8 +329,11 @@ __global__ __launch_bounds__(kThreads) void varint_size_kernel(const int64_t* __
     const uint32_t c = blockIdx.x, row = blockIdx.y;
     const uint64_t e0 = (uint64_t)c * kEncChunk;
     uint64_t n = 0;
-    for (uint32_t i = threadIdx.x; i < kEncChunk; i += kThreads)
-        if (e0 + i < len) n += varint_size(vals[row * stride + e0 + i]);
+#pragma unroll
+    for (uint32_t q = 0; q < kEncPer; ++q) {
+        const uint64_t e = e0 + q * kThreads + threadIdx.x;
+        if (e < len) n += varint_size(vals[row * stride + e]);
+    }
     __shared__ uint64_t red[kThreads / 64];
     for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n;
@@ -341,46 +345,79 @@ __global__ __launch_bounds__(kThreads) void varint_size_kernel(const int64_t* __
     }
 }
 
-// write: the block assembles its chunk's bytes in LDS (<= 10 B per element), then stores them
-// at the chunk's byte offset (chunk_off = row offset + exclusive scan of chunk_bytes).
+// inverse of leb_pack8: 7-bit groups of z -> bytes (group i in byte i), continuation bits not set
+__device__ __forceinline__ uint64_t leb_spread8(uint64_t z) {
+    uint64_t x = z & 0x00FFFFFFFFFFFFFFull;
+    x = (x & 0x000000000FFFFFFFull) | ((x & 0x00FFFFFFF0000000ull) << 4);
+    x = (x & 0x00003FFF00003FFFull) | ((x & 0x0FFFC0000FFFC000ull) << 2);
+    x = (x & 0x007F007F007F007Full) | ((x & 0x3F803F803F803F80ull) << 1);
+    return x;
+}
+
+// write: coalesced loads (element q * 256 + t of the chunk), one block-wide scan of the sizes per
+// q, bytes assembled in LDS at the chunk's global byte offset mod 4 (so LDS dwords line up with
+// global dwords), then dword stores for the interior and byte stores for the two partial ends
+// (shared with the neighbouring chunks).  chunk_off = row offset + exclusive scan of chunk_bytes.
 __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* __restrict__ vals, uint64_t len,
                                                                 uint64_t stride, uint32_t chunks,
                                                                 const uint64_t* __restrict__ chunk_off,
                                                                 uint8_t* __restrict__ dst) {
     const uint32_t c = blockIdx.x, row = blockIdx.y;
     const uint64_t e0 = (uint64_t)c * kEncChunk;
-    constexpr uint32_t PER = kEncChunk / kThreads;            // 16 consecutive elements per thread
-    __shared__ uint8_t buf[kEncChunk * 10];
-    __shared__ uint32_t tsum[kThreads];
-    int64_t v[PER];
-    uint32_t sz = 0;
+    __shared__ uint32_t buf[(kEncChunk * 10 + 8) / 4];
+    __shared__ uint32_t wsum[kThreads / 64];
+    const uint64_t go = chunk_off[(uint64_t)row * chunks + c];
+    const uint32_t lead = (uint32_t)(go & 3);
+    uint8_t* b8 = reinterpret_cast<uint8_t*>(buf);
+    int64_t v[kEncPer];
 #pragma unroll
-    for (uint32_t q = 0; q < PER; ++q) {
-        const uint64_t e = e0 + threadIdx.x * PER + q;
+    for (uint32_t q = 0; q < kEncPer; ++q) {
+        const uint64_t e = e0 + q * kThreads + threadIdx.x;
         v[q] = e < len ? vals[row * stride + e] : 0;
-        sz += e < len ? varint_size(v[q]) : 0;
     }
-    tsum[threadIdx.x] = sz;
-    __syncthreads();
-    for (int o = 1; o < kThreads; o <<= 1) {
-        const uint32_t add = threadIdx.x >= (uint32_t)o ? tsum[threadIdx.x - o] : 0;
-        __syncthreads();
-        tsum[threadIdx.x] += add;
-        __syncthreads();
-    }
-    uint32_t w = tsum[threadIdx.x] - sz;
-    const uint32_t total = tsum[kThreads - 1];
+    uint32_t base = lead;
 #pragma unroll
-    for (uint32_t q = 0; q < PER; ++q) {
-        const uint64_t e = e0 + threadIdx.x * PER + q;
-        if (e >= len) break;
-        uint64_t z = ((uint64_t)v[q] << 1) ^ (uint64_t)(v[q] >> 63);
-        while (z >= 0x80) { buf[w++] = (uint8_t)(z | 0x80); z >>= 7; }
-        buf[w++] = (uint8_t)z;
+    for (uint32_t q = 0; q < kEncPer; ++q) {
+        const bool in = e0 + q * kThreads + threadIdx.x < len;
+        const uint64_t z = ((uint64_t)v[q] << 1) ^ (uint64_t)(v[q] >> 63);
+        const uint32_t n = in ? varint_size(v[q]) : 0u;
+        uint32_t incl = n;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o);
+            if ((threadIdx.x & 63) >= (uint32_t)o) incl += t;
+        }
+        __syncthreads();                                     // wsum of the previous q consumed
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        uint32_t off = base + incl - n, total = 0;
+        for (uint32_t w = 0; w < kThreads / 64; ++w) {
+            if (w < (threadIdx.x >> 6)) off += wsum[w];
+            total += wsum[w];
+        }
+        base += total;
+        // bytes: groups 0..7 from the spread, continuation bit on every byte but the last
+        const uint64_t lo = leb_spread8(z);
+        const uint32_t g8 = (uint32_t)(z >> 56) & 0x7Fu, g9 = (uint32_t)(z >> 63);
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i)
+            if (i < n) b8[off + i] = (uint8_t)(i + 1 < n ? (lo >> (8 * i)) | 0x80 : (lo >> (8 * i)) & 0x7F);
+        if (n > 8) b8[off + 8] = (uint8_t)(g8 | (n > 9 ? 0x80u : 0u));
+        if (n > 9) b8[off + 9] = (uint8_t)g9;
     }
     __syncthreads();
-    uint8_t* o = dst + chunk_off[(uint64_t)row * chunks + c];
-    for (uint32_t i = threadIdx.x; i < total; i += kThreads) o[i] = buf[i];
+    const uint32_t end = base;                               // lead + chunk bytes
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + (go & ~3ull));
+    uint8_t* d8 = dst + (go & ~3ull);
+    const uint32_t nw = (end + 3) / 4;
+    for (uint32_t k = threadIdx.x; k < nw; k += kThreads) {
+        const uint32_t lo = k * 4, hi = lo + 4;
+        if (lo >= lead && hi <= end) {
+            d32[k] = buf[k];
+        } else {
+            for (uint32_t i = lo; i < hi; ++i)
+                if (i >= lead && i < end) d8[i] = b8[i];
+        }
+    }
 }
 
 // exclusive scan of chunk_bytes per row (one block per row) + row base; row_bytes = total
