@@ -340,6 +340,14 @@ def main():
                                                   seed=seed, payload_ptr=pay.data_ptr(), payload_cap=cap,
                                                   stream=stream())
             pt.record(f) if i else f()
+        pct = Timer(torch)
+        for i in range(3):
+            f = lambda: eng.participant_share_dev(msk, sch, sec.data_ptr(), Dp, drw.data_ptr(), sh.data_ptr(),  # noqa
+                                                  seed=seed, payload_ptr=pay.data_ptr(), payload_cap=cap,
+                                                  mode=E.REVEAL_CANONICAL, stream=stream())
+            pct.record(f) if i else f()
+        eng.participant_share_dev(msk, sch, sec.data_ptr(), Dp, drw.data_ptr(), sh.data_ptr(), seed=seed,
+                                  stream=stream())       # the exact shares again for the round trip below
         idx = list(range(n - 1, n - 1 - (t + k), -1))
         sub = sh[idx].contiguous()
         out = torch.empty(Dp, dtype=torch.int64, device=dev)
@@ -356,10 +364,11 @@ def main():
             f = lambda: eng.recipient_reveal_dev(msk, seeds.data_ptr(), Ns, 4, sch, Dp, idx, sub.data_ptr(), B, p,  # noqa
                                                  out.data_ptr(), Dp, stream=stream())
             rt.record(f) if i else f()
-        p_ms, r_ms = pt.mean_ms(), rt.mean_ms()
+        p_ms, r_ms, pc_ms = pt.mean_ms(), rt.mean_ms(), pct.mean_ms()
         side["pipelines"] = {
             "config": f"configs[4] per GPU: ChaCha(128-bit) masking + PackedShamir k=8 n=26 t=7 at {Dp:,}-dim",
             "participant_ms": p_ms, "participant_secrets_per_s": Dp / (p_ms * 1e-3),
+            "participant_canonical_ms": pc_ms,
             "recipient_seeds": Ns, "recipient_ms": r_ms,
             "recipient_mask_elems_per_s": Ns * Dp / (r_ms * 1e-3),
         }

@@ -264,11 +264,13 @@ sda_status sda_recipient_reveal(sda_engine* h, const sda_masking_scheme* ms,
 /* Participant (participate.rs:53-76): SecretMasker::mask -> ShareGenerator::generate -> per-clerk
  * payload encoding (sodium.rs:36-41) on device.  seed: host words (ChaCha); full_masks: device [D]
  * (Full); secrets [D], draws (as sda_share_generate) and shares_out [n][B] are device buffers.
+ * mode: packed shares as tss' signed values (SDA_REVEAL_EXACT) or canonical residues
+ * (SDA_REVEAL_CANONICAL, see sda_packed_generate_mode_dev); ignored for Additive.
  * payload (device, may be NULL): the n clerk payloads back to back, payload_row_bytes[n] (host). */
 sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms, const uint32_t* seed,
                                      uint64_t seed_words, const int64_t* full_masks,
                                      const sda_sharing_scheme* ss, const int64_t* secrets, uint64_t dimension,
-                                     const int64_t* draws, int64_t* shares_out, uint8_t* payload,
+                                     const int64_t* draws, int32_t mode, int64_t* shares_out, uint8_t* payload,
                                      uint64_t payload_cap, uint64_t* payload_row_bytes, void* stream);
 
 /* Synthetic benchmark input: dst[r*cols + c] = lo + splitmix64(seed, r, c) % (hi - lo). */

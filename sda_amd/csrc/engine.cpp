@@ -983,7 +983,7 @@ sda_status sda_recipient_reveal(sda_engine* h, const sda_masking_scheme* ms, con
 sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms, const uint32_t* seed,
                                      uint64_t seed_words, const int64_t* full_masks, const sda_sharing_scheme* ss,
                                      const int64_t* secrets, uint64_t dimension, const int64_t* draws,
-                                     int64_t* shares_out, uint8_t* payload, uint64_t payload_cap,
+                                     int32_t mode, int64_t* shares_out, uint8_t* payload, uint64_t payload_cap,
                                      uint64_t* payload_row_bytes, void* stream) {
     if (!h || !ms || !ss || (dimension && (!secrets || !shares_out)) || (payload && !payload_row_bytes))
         return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
@@ -992,6 +992,7 @@ sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms
     const uint64_t D = dimension;
     const bool packed = ss->kind == SDA_SHARING_PACKED_SHAMIR;
     if (!packed && ss->kind != SDA_SHARING_ADDITIVE) return fail(SDA_ERR_INVALID_ARGUMENT, "unknown sharing scheme kind");
+    if (mode != SDA_REVEAL_EXACT && mode != SDA_REVEAL_CANONICAL) return fail(SDA_ERR_INVALID_ARGUMENT, "bad mode");
     if (packed) {
         if (sda_status e = check_packed(ss)) return e;
     } else {
@@ -1027,7 +1028,7 @@ sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms
         if (!draws) return fail(SDA_ERR_INVALID_ARGUMENT, "need the randomness draws");
         if (packed) {
             if (sda_status e = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return e;
-            sda::PackedGenArgs ga{masked, D, 1, draws, shares_out};
+            sda::PackedGenArgs ga{masked, D, 1, draws, shares_out, mode == SDA_REVEAL_CANONICAL};
             HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)ss->secret_count, (uint32_t)ss->privacy_threshold,
                                                 (uint32_t)n, (uint32_t)ss->modulus, (uint32_t)ss->omega_secrets,
                                                 (uint32_t)ss->omega_shares, h->gen_tab, h->gen_log, st));

@@ -101,8 +101,8 @@ SIGNATURES = [
                                    C.POINTER(S.SharingSchemeC), C.c_uint64, _u64p, C.POINTER(_i64p), _u64p,
                                    C.c_uint64, C.c_int64, C.c_int32, _i64p, C.c_uint64, _u64p]),
     ("sda_participant_share_dev", _st, [_vp, C.POINTER(S.MaskingSchemeC), _u32p, C.c_uint64, _vp,
-                                        C.POINTER(S.SharingSchemeC), _vp, C.c_uint64, _vp, _vp, _vp, C.c_uint64,
-                                        _u64p, _vp]),
+                                        C.POINTER(S.SharingSchemeC), _vp, C.c_uint64, _vp, C.c_int32, _vp, _vp,
+                                        C.c_uint64, _u64p, _vp]),
 ]
 
 _lib = None
@@ -365,13 +365,13 @@ class Engine:
         return olen.value
 
     def participant_share_dev(self, masking, sharing, secrets_ptr, dimension, draws_ptr, shares_ptr, seed=None,
-                              full_masks_ptr=None, payload_ptr=None, payload_cap=0, stream=None):
+                              full_masks_ptr=None, payload_ptr=None, payload_cap=0, mode=REVEAL_EXACT, stream=None):
         """participate.rs:53-76 (+ payload encoding) on device; returns per-clerk payload byte counts."""
         ms, ss = masking.c(), sharing.c()
         sd = _arr(seed if seed is not None else [], np.uint32)
         n = sharing.output_size()
         rb = np.zeros(max(n, 1), np.uint64)
         _check(self.lib.sda_participant_share_dev(self.h, C.byref(ms), _ptr(sd, _u32p), sd.size, full_masks_ptr,
-                                                  C.byref(ss), secrets_ptr, dimension, draws_ptr, shares_ptr,
+                                                  C.byref(ss), secrets_ptr, dimension, draws_ptr, mode, shares_ptr,
                                                   payload_ptr, payload_cap, _ptr(rb, _u64p), stream))
         return rb[:n]

@@ -110,8 +110,9 @@ def test_participant_share_dev(engine, oracle, ms, ss):
         assert host[off[c]:off[c + 1]] == oracle.varint_encode(exp[c])
 
 
-@pytest.mark.parametrize("mode", [E.REVEAL_EXACT, E.REVEAL_CANONICAL])
-def test_aggregation_end_to_end_on_device(engine, mode):
+@pytest.mark.parametrize("gen_mode", [E.REVEAL_EXACT, E.REVEAL_CANONICAL], ids=["gen_exact", "gen_canon"])
+@pytest.mark.parametrize("mode", [E.REVEAL_EXACT, E.REVEAL_CANONICAL], ids=["rev_exact", "rev_canon"])
+def test_aggregation_end_to_end_on_device(engine, mode, gen_mode):
     """participants (device) -> clerks: decode + combine their payloads (device) -> recipient reveal
     (device) == sum of the inputs mod p (integration-tests/tests/full_loop.rs's property at scale)."""
     ms, ss = S.ChaChaMasking(P, 80_000, 128), S.CONFIG_PACKED
@@ -128,7 +129,7 @@ def test_aggregation_end_to_end_on_device(engine, mode):
         sh = torch.empty((n, B), dtype=torch.int64, device="cuda")
         pay = torch.zeros(cap, dtype=torch.uint8, device="cuda")
         rb = engine.participant_share_dev(ms, ss, sec.data_ptr(), D, dr.data_ptr(), sh.data_ptr(), seed=seed,
-                                          payload_ptr=pay.data_ptr(), payload_cap=cap)
+                                          payload_ptr=pay.data_ptr(), payload_cap=cap, mode=gen_mode)
         off = np.concatenate([[0], np.cumsum(rb)]).astype(np.int64)
         h = pay.cpu().numpy().tobytes()
         payloads.append([h[off[c]:off[c + 1]] for c in range(n)])
