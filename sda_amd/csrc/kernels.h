@@ -48,7 +48,10 @@ struct PackedGenArgs {
     const int64_t* secrets; uint64_t dimension; uint64_t n_vectors;
     const int64_t* draws; int64_t* out;
     bool canonical = false;       // shares as canonical residues in [0, p) instead of tss' signed values
+    uint32_t prime = 0;           // set by launch_packed_generate (selects the lazy-truncation kernel)
 };
+// Exact share-gen uses lazy truncation (packed_gen.hip: Trunc<true>) for primes at least this big.
+constexpr uint32_t kLazyTruncMinP = 1u << 24;
 // Batches whose inputs fall outside (-p, p) are logged by the fast kernel and recomputed by a
 // generic exact fix-up kernel.  `log_buf` is device memory of packed_gen_log_bytes() bytes.
 constexpr uint32_t kGenLogCap = 1u << 16;

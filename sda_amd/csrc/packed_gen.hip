@@ -20,23 +20,86 @@ struct FE {
     uint32_t c;
 };
 
+// Rust `v % p` from the canonical residue c and the sign word sw of the exact dividend v.
+//   exact (LAZY = false): trunc_rep, 5 VALU ops incl. the c == 0 case (v < 0, v = 0 mod p -> 0);
+//   LAZY: c - (p & sign), 3 ops, which gives -p instead of 0 exactly when v < 0 and v = 0 mod p
+//   (a nonzero multiple of p: probability ~1/p per value; v == 0 itself is exact).  -p is the only
+//   value outside (-p, p), so a running signed min over the outputs finds it (one v_min3 per two
+//   values, as opaque asm so the compiler cannot reassociate the chain and stretch live ranges);
+//   such a batch is not stored but logged for the generic exact fix-up kernel.  x * len_inv
+//   needs no check (v = 0 mod p only when x = 0).  LAZY is launched only for p >= 2^24.
+template <bool LAZY>
+struct Trunc {
+    int32_t smin = 0x7FFFFFFF;
+    __device__ __forceinline__ int32_t operator()(uint32_t c, uint32_t sw, uint32_t p) {
+        if constexpr (LAZY) {
+            int32_t s = (int32_t)(c - (p & (uint32_t)((int32_t)sw >> 31)));
+            asm("" : "+v"(s));        // opaque: keeps isel from widening the residue chain
+            return s;
+        }
+        else return trunc_rep(c, sw, p);
+    }
+    __device__ __forceinline__ void note2(int32_t a, int32_t b) {
+        if constexpr (LAZY) asm("v_min3_i32 %0, %1, %2, %3" : "=v"(smin) : "v"(smin), "v"(a), "v"(b));
+    }
+    static constexpr bool lazy = LAZY;
+    __device__ __forceinline__ bool bad(uint32_t p) const { return LAZY && smin == -(int32_t)p; }
+};
+
+// Montgomery product with a uniform (SGPR) multiplier as a fixed instruction sequence:
+// v_mad_u64_u32 (T = a' x [+ acc]), v_mul_lo_u32 (u = T pinv), v_mad_u64_u32 (T + u p) -> high word
+// in [0, 2p).  (Left to isel, the exact kernel's lazy variant grew a dead mov + mad-by-0 after
+// every reduction.)
+__device__ __forceinline__ uint64_t mad_su(uint32_t s, uint32_t v, uint64_t acc) {
+    uint64_t r, cy;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cy) : "s"(s), "v"(v), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ uint64_t mul_su(uint32_t s, uint32_t v) {
+    uint64_t r, cy;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cy) : "s"(s), "v"(v));
+    return r;
+}
+__device__ __forceinline__ uint32_t redc_su(uint64_t T, const MontP& M) {
+    const uint32_t u = (uint32_t)T * M.pinv;
+    return (uint32_t)(mad_su(M.p, u, T) >> 32);
+}
+// a' x mod p in [0, p) (a' uniform, Montgomery form); ASM selects the fixed sequence above
+// (used by the lazy kernel; the exact-trunc kernel keeps the compiler's, which allocates better).
+template <bool ASM>
+__device__ __forceinline__ uint32_t montu(uint32_t a_m, uint32_t x, const MontP& M) {
+    if constexpr (ASM) return red1(redc_su(mul_su(a_m, x), M), M.p);
+    else return red1(redc_lazy((uint64_t)a_m * x, M), M.p);
+}
+// (a' x + b' y) mod p in [0, p)   (a' x + b' y < 2 p^2 < p R)
+template <bool ASM>
+__device__ __forceinline__ uint32_t montu2(uint32_t a_m, uint32_t x, uint32_t b_m, uint32_t y, const MontP& M) {
+    if constexpr (ASM) return red1(redc_su(mad_su(b_m, y, mul_su(a_m, x)), M), M.p);
+    else return red1(redc_lazy((uint64_t)a_m * x + (uint64_t)b_m * y, M), M.p);
+}
+
 // radix-2 butterfly (u ± w c) % p.  The signs come from the exact i64 dividends (one
 // v_mad_i64_i32 each), the residues from one lazy Montgomery product shared by both outputs.
-__device__ __forceinline__ void bfly2(FE& u, FE& c, int32_t w, int32_t nw, uint32_t w_m, const MontP& M) {
+
+template <class TR>
+__device__ __forceinline__ void bfly2(FE& u, FE& c, int32_t w, int32_t nw, uint32_t w_m, const MontP& M, TR& tr) {
     const int64_t v1 = (int64_t)u.s + (int64_t)w * c.s;
     const int64_t v2 = (int64_t)u.s + (int64_t)nw * c.s;
-    const uint32_t tc = red1(redc_lazy((uint64_t)w_m * c.c, M), M.p);
+    const uint32_t tc = montu<TR::lazy>(w_m, c.c, M);
     const uint32_t c1 = addm(u.c, tc, M.p), c2 = subm(u.c, tc, M.p);
-    u = FE{trunc_rep(c1, hi32(v1), M.p), c1};
-    c = FE{trunc_rep(c2, hi32(v2), M.p), c2};
+    u = FE{tr(c1, hi32(v1), M.p), c1};
+    c = FE{tr(c2, hi32(v2), M.p), c2};
+    tr.note2(u.s, c.s);
 }
 
 // twiddle omega^0 = 1: (u + c) % p, (u - c) % p.  A saturating add keeps the exact sum's sign.
-__device__ __forceinline__ void bfly2_unit(FE& u, FE& c, uint32_t p) {
+template <class TR>
+__device__ __forceinline__ void bfly2_unit(FE& u, FE& c, uint32_t p, TR& tr) {
     const uint32_t c1 = addm(u.c, c.c, p), c2 = subm(u.c, c.c, p);
     const int32_t s1 = __builtin_elementwise_add_sat(u.s, c.s), s2 = __builtin_elementwise_sub_sat(u.s, c.s);
-    u = FE{trunc_rep(c1, (uint32_t)s1, p), c1};
-    c = FE{trunc_rep(c2, (uint32_t)s2, p), c2};
+    u = FE{tr(c1, (uint32_t)s1, p), c1};
+    c = FE{tr(c2, (uint32_t)s2, p), c2};
+    tr.note2(u.s, c.s);
 }
 
 // Compile-time map of the radix-3 registers that hold a known zero (the zero padding of
@@ -113,7 +176,7 @@ __device__ __forceinline__ void transform_canon(const int64_t (&raw)[L], const G
                         y[g + i + th] = addm(bb, E, p);
                         y[g + i + 2 * th] = subm(subm(bb, C, p), E, p);
                     } else {
-                        const uint32_t Dd = (i == 0) ? y[g + i + 2 * th] : mont(T.sq3_m[OB + i], y[g + i + 2 * th]);
+                        const uint32_t Dd = (i == 0) ? y[g + i + 2 * th] : mont(T.tw3_m[OB + (2 * i) % LEN], y[g + i + 2 * th]);
                         const uint32_t E = mont(w3, subm(C, Dd, p));
                         y[g + i] = addm(addm(bb, C, p), Dd, p);
                         y[g + i + th] = addm(subm(bb, Dd, p), E, p);
@@ -134,8 +197,8 @@ __device__ __forceinline__ void transform_canon(const int64_t (&raw)[L], const G
 // per row pair (13 dwordx4 instead of 26 dwordx2 at n = 26) when WIDE (B even, 16-B aligned out).
 // (A persistent grid-stride variant was measured slower: the loop made hipcc keep the twiddle
 // words in SGPRs across tiles and spill.)
-template <int L, int N3, bool WIDE, bool CANON>
-__global__ __launch_bounds__(gen_block<L>()) __attribute__((amdgpu_waves_per_eu(SDA_GEN_WAVES)))
+template <int L, int N3, bool WIDE, bool CANON, bool LAZY>
+__global__ __launch_bounds__(gen_block<L>()) __attribute__((amdgpu_waves_per_eu(SDA_GEN_WAVES, SDA_GEN_WAVES)))
 void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const int64_t* __restrict__ draws,
                        int64_t* __restrict__ out, uint32_t k, uint32_t t, uint64_t B,
                        const GenTables* __restrict__ Tp, unsigned int* __restrict__ log) {
@@ -218,12 +281,13 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         // to the generic path from inside this loop would force the live FFT state to spill.)
         const uint32_t ok = in_range ? 1u : 0u;
         const auto okx = __builtin_amdgcn_permlane32_swap(ok, ok, false, false);
-        const bool pair_ok = in_range && (half ? okx[0] : okx[1]);
+        bool pair_ok = in_range && (half ? okx[0] : okx[1]);
         if (live && !pair_ok) {                  // -> packed_gen_fixup_kernel
             const uint32_t slot = atomicAdd(log, 1u);
             if (slot < kGenLogCap) reinterpret_cast<uint64_t*>(log + 16)[slot] = (uint64_t)vec * B + b;
         }
 
+        Trunc<LAZY> tr;
         int32_t ys[N3];                  // shares (tss' signed values, or canonical residues)
         if constexpr (CANON) {
             transform_canon<L, N3>(raw, T, M, ys);
@@ -239,18 +303,18 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
             static_for<0, L, LEN>([&](auto g) {
                 static_for<0, H>([&](auto i) {
                     if constexpr (i == 0) {
-                        bfly2_unit(x[g], x[g + H], p);
+                        bfly2_unit(x[g], x[g + H], p, tr);
                     } else {
                         const int32_t w = (int32_t)T.tw2[H - 1 + i];
-                        bfly2(x[g + i], x[g + i + H], w, -w, T.tw2_m[H - 1 + i], M);
+                        bfly2(x[g + i], x[g + i + H], w, -w, T.tw2_m[H - 1 + i], M, tr);
                     }
                 });
             });
         });
         // x * len_inv % p   (len_inv > 0 => the exact product has the sign of x)
         static_for<0, L>([&](auto i) {
-            const uint32_t c = red1(redc_lazy((uint64_t)T.linv_m * x[i].c, M), p);
-            x[i] = FE{trunc_rep(c, (uint32_t)x[i].s, p), c};
+            const uint32_t c = montu<LAZY>(T.linv_m, x[i].c, M);
+            x[i] = FE{tr(c, (uint32_t)x[i].s, p), c};
         });
 
         // ---- fft3: radix-3 DIT over omega_shares on digit-reversed, zero-extended registers ----
@@ -281,34 +345,53 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                                 // x = x^2 = 1: (b + c + d) % p
                                 if constexpr (zd) {
                                     const uint32_t c = addm(bb.c, cc.c, p);
-                                    r[q] = FE{trunc_rep(c, (uint32_t)__builtin_elementwise_add_sat(bb.s, cc.s), p), c};
+                                    r[q] = FE{tr(c, (uint32_t)__builtin_elementwise_add_sat(bb.s, cc.s), p), c};
                                 } else {
                                     const int64_t v = (int64_t)bb.s + cc.s + dd.s;
                                     const uint32_t c = addm(addm(bb.c, cc.c, p), dd.c, p);
-                                    r[q] = FE{trunc_rep(c, hi32(v), p), c};
+                                    r[q] = FE{tr(c, hi32(v), p), c};
                                 }
                             } else if constexpr (zd) {
                                 const int32_t xw = (int32_t)T.tw3[OB + j];
                                 const int64_t v = (int64_t)bb.s + (int64_t)xw * cc.s;
-                                const uint32_t c = addm(bb.c, red1(redc_lazy((uint64_t)T.tw3_m[OB + j] * cc.c, M), p), p);
-                                r[q] = FE{trunc_rep(c, hi32(v), p), c};
+                                const uint32_t c = addm(bb.c, montu<LAZY>(T.tw3_m[OB + j], cc.c, M), p);
+                                r[q] = FE{tr(c, hi32(v), p), c};
                             } else {
                                 // twiddles < p < 2^31: signed 32x32 products are exact (v_mad_i64_i32)
-                                const int32_t xw = (int32_t)T.tw3[OB + j], x2 = (int32_t)T.sq3[OB + j];
+                                // x^2 % p = omega_len^(2j mod len): the same level's entry (2j) % len, so
+                                // the stage needs half the uniform words (fewer SGPR spills)
+                                constexpr int j2 = (2 * j) % LEN;
+                                const int32_t xw = (int32_t)T.tw3[OB + j], x2 = (int32_t)T.tw3[OB + j2];
                                 const int64_t v = (int64_t)bb.s + (int64_t)xw * cc.s + (int64_t)x2 * dd.s;
-                                // residue: REDC(x' C + x2' D) + B    (x' C + x2' D < 2 p^2 < p R)
-                                const uint64_t acc = (uint64_t)T.tw3_m[OB + j] * cc.c + (uint64_t)T.sq3_m[OB + j] * dd.c;
-                                const uint32_t c = addm(bb.c, red1(redc_lazy(acc, M), p), p);
-                                r[q] = FE{trunc_rep(c, hi32(v), p), c};
+                                // residue: REDC(x' C + x2' D) + B
+                                const uint32_t c = addm(bb.c, montu2<LAZY>(T.tw3_m[OB + j], cc.c, T.tw3_m[OB + j2], dd.c, M), p);
+                                r[q] = FE{tr(c, hi32(v), p), c};
                             }
                         });
                         y[g + i] = r[0]; y[g + i + th] = r[1]; y[g + i + 2 * th] = r[2];
+                        tr.note2(r[0].s, r[1].s);
+                        tr.note2(r[2].s, r[2].s);
                     }
                 });
             });
         });
 
         static_for<0, N3>([&](auto j) { ys[j] = y[j].s; });
+        }
+
+        if constexpr (LAZY) {                    // a -p under lazy truncation (see Trunc): same rule
+            const uint32_t z = tr.bad(p) ? 1u : 0u;
+            const auto zx = __builtin_amdgcn_permlane32_swap(z, z, false, false);
+            const bool pair_zero = z || (half ? zx[0] : zx[1]);
+            if (pair_ok && pair_zero) {
+                pair_ok = false;
+                if (live) {
+                    const uint32_t slot = atomicAdd(log, 1u);
+                    if (slot < kGenLogCap)
+                        reinterpret_cast<uint64_t*>(log + 16)[slot] =
+                            (uint64_t)blockIdx.y * B + (uint64_t)blockIdx.x * BS + lb;
+                }
+            }
         }
 
         // ---- shares = points[1..=n], clerk-major (batched.rs:46-48) ----
@@ -338,15 +421,19 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
 
 template <int L, int N3, bool CANON>
 static void gen_launch_mode(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
-                            const GenFixupLog& log, hipStream_t s) {
+                            uint32_t p, const GenFixupLog& log, hipStream_t s) {
     constexpr int BS = gen_block<L>();
     const dim3 grid((unsigned)((B + BS - 1) / BS), (unsigned)a.n_vectors);
-    if (B % 2 == 0 && ((uintptr_t)a.out % 16) == 0)
-        hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, CANON>), grid, dim3(BS), 0, s, a.secrets, a.dimension,
-                           a.draws, a.out, k, t, B, T, log.count);
+    const bool wide = B % 2 == 0 && ((uintptr_t)a.out % 16) == 0;
+    if (wide && !CANON && p >= kLazyTruncMinP)          // exact shares, lazy zero handling
+        hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, false, true>), grid, dim3(BS), 0, s, a.secrets,
+                           a.dimension, a.draws, a.out, k, t, B, T, log.count);
+    else if (wide)
+        hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, CANON, false>), grid, dim3(BS), 0, s, a.secrets,
+                           a.dimension, a.draws, a.out, k, t, B, T, log.count);
     else
-        hipLaunchKernelGGL((packed_gen_kernel<L, N3, false, CANON>), grid, dim3(BS), 0, s, a.secrets, a.dimension,
-                           a.draws, a.out, k, t, B, T, log.count);
+        hipLaunchKernelGGL((packed_gen_kernel<L, N3, false, CANON, false>), grid, dim3(BS), 0, s, a.secrets,
+                           a.dimension, a.draws, a.out, k, t, B, T, log.count);
 }
 
 template <int L, int N3>
@@ -354,8 +441,9 @@ static hipError_t gen_launch(const PackedGenArgs& a, uint32_t k, uint32_t t, uin
                              const GenFixupLog& log, hipStream_t s) {
     constexpr int BS = gen_block<L>();
     if ((B + BS - 1) / BS > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    if (a.canonical) gen_launch_mode<L, N3, true>(a, k, t, B, T, log, s);
-    else gen_launch_mode<L, N3, false>(a, k, t, B, T, log, s);
+    const uint32_t p = a.prime;
+    if (a.canonical) gen_launch_mode<L, N3, true>(a, k, t, B, T, p, log, s);
+    else gen_launch_mode<L, N3, false>(a, k, t, B, T, p, log, s);
     return hipGetLastError();
 }
 
@@ -457,9 +545,11 @@ __global__ __launch_bounds__(256) void packed_gen_fixup_kernel(const int64_t* __
 
 size_t packed_gen_log_bytes() { return 64 + (size_t)kGenLogCap * sizeof(uint64_t); }
 
-hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t, uint32_t n, uint32_t p,
+hipError_t launch_packed_generate(const PackedGenArgs& args, uint32_t k, uint32_t t, uint32_t n, uint32_t p,
                                   uint32_t omega_secrets, uint32_t omega_shares, DeviceTable& tab, void* log_buf,
                                   hipStream_t s) {
+    PackedGenArgs a = args;
+    a.prime = p;
     const uint32_t L = k + t + 1, N3 = n + 1;
     const uint64_t B = (a.dimension + k - 1) / k;
     if (B == 0 || a.n_vectors == 0) return hipSuccess;

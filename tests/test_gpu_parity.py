@@ -332,3 +332,47 @@ def test_packed_generate_canonical_mode(engine, oracle, sch):
         got = out.cpu().numpy()
         assert_same(got[:, :B], exp)
         assert got.min() >= 0
+
+
+def _bitrev(i, bits):
+    return int(format(i, f"0{bits}b")[::-1], 2) if bits else 0
+
+
+@pytest.mark.parametrize("sch", [s for s in packed_schemes() if s.prime_modulus >= 2**24 and
+                                 s.secret_count + s.privacy_threshold() + 1 >= 4],
+                         ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")
+def test_packed_generate_negative_multiple_of_p(engine, oracle, sch):
+    """Exact share-gen where a first-stage dividend is exactly -p (tss: `-p % p == 0`).
+
+    The exact kernel for p >= 2^24 truncates lazily (packed_gen.hip: Trunc<true>) and must send
+    such batches to the generic fix-up; every other batch stays on the fast path.  The traps sit
+    in the radix-2 stage-1 butterflies (x[2m] +- x[2m+1] over bit-reversed inputs).
+    """
+    p, k, t = sch.prime_modulus, sch.secret_count, sch.privacy_threshold()
+    L = k + t + 1
+    lb = L.bit_length() - 1
+    rng = np.random.default_rng(p % 4099 + L)
+    B = 96
+    D = B * k
+    secrets = rng.integers(-(p - 1), p, size=D, dtype=np.int64)
+    draws = rng.integers(0, p - 1, size=B * t, dtype=np.int64)
+
+    def put(b, r, v):          # raw index r of batch b: [0, secrets(k), randomness(t)]
+        if r <= k:
+            secrets[b * k + r - 1] = v
+        else:
+            draws[b * t + r - 1 - k] = v
+
+    for b in range(0, B, 3):   # two of three batches trapped, the rest stay random
+        if b + 1 < B:
+            b_list = (b, b + 1)
+        else:
+            b_list = (b,)
+        for bb in b_list:
+            m = int(rng.integers(1, L // 2))
+            u, c = _bitrev(2 * m, lb), _bitrev(2 * m + 1, lb)
+            a = int(rng.integers(1, p))
+            put(bb, u, -a)
+            put(bb, c, (p - a) if bb % 2 else -(p - a))     # u - c == -p   /   u + c == -p
+    got = engine.share_generate(sch, secrets, draws)
+    assert_same(got, oracle.packed_generate(_pp(oracle, sch), secrets, draws))
