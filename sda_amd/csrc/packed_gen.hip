@@ -20,64 +20,6 @@ struct FE {
     uint32_t c;
 };
 
-// Rust `v % p` from the canonical residue c and the sign word sw of the exact dividend v.
-//   exact (LAZY = false): trunc_rep, 5 VALU ops incl. the c == 0 case (v < 0, v = 0 mod p -> 0);
-//   LAZY: c - (p & sign), 3 ops, which gives -p instead of 0 exactly when v < 0 and v = 0 mod p
-//   (a nonzero multiple of p: probability ~1/p per value; v == 0 itself is exact).  -p is the only
-//   value outside (-p, p), so a running signed min over the outputs finds it (one v_min3 per two
-//   values, as opaque asm so the compiler cannot reassociate the chain and stretch live ranges);
-//   such a batch is not stored but logged for the generic exact fix-up kernel.  x * len_inv
-//   needs no check (v = 0 mod p only when x = 0).  LAZY is launched only for p >= 2^24.
-template <bool LAZY>
-struct Trunc {
-    int32_t smin = 0x7FFFFFFF;
-    __device__ __forceinline__ int32_t operator()(uint32_t c, uint32_t sw, uint32_t p) {
-        if constexpr (LAZY) {
-            int32_t s = (int32_t)(c - (p & (uint32_t)((int32_t)sw >> 31)));
-            asm("" : "+v"(s));        // opaque: keeps isel from widening the residue chain
-            return s;
-        }
-        else return trunc_rep(c, sw, p);
-    }
-    __device__ __forceinline__ void note2(int32_t a, int32_t b) {
-        if constexpr (LAZY) asm("v_min3_i32 %0, %1, %2, %3" : "=v"(smin) : "v"(smin), "v"(a), "v"(b));
-    }
-    static constexpr bool lazy = LAZY;
-    __device__ __forceinline__ bool bad(uint32_t p) const { return LAZY && smin == -(int32_t)p; }
-};
-
-// Montgomery product with a uniform (SGPR) multiplier as a fixed instruction sequence:
-// v_mad_u64_u32 (T = a' x [+ acc]), v_mul_lo_u32 (u = T pinv), v_mad_u64_u32 (T + u p) -> high word
-// in [0, 2p).  (Left to isel, the exact kernel's lazy variant grew a dead mov + mad-by-0 after
-// every reduction.)
-__device__ __forceinline__ uint64_t mad_su(uint32_t s, uint32_t v, uint64_t acc) {
-    uint64_t r, cy;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cy) : "s"(s), "v"(v), "v"(acc));
-    return r;
-}
-__device__ __forceinline__ uint64_t mul_su(uint32_t s, uint32_t v) {
-    uint64_t r, cy;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cy) : "s"(s), "v"(v));
-    return r;
-}
-__device__ __forceinline__ uint32_t redc_su(uint64_t T, const MontP& M) {
-    const uint32_t u = (uint32_t)T * M.pinv;
-    return (uint32_t)(mad_su(M.p, u, T) >> 32);
-}
-// a' x mod p in [0, p) (a' uniform, Montgomery form); ASM selects the fixed sequence above
-// (used by the lazy kernel; the exact-trunc kernel keeps the compiler's, which allocates better).
-template <bool ASM>
-__device__ __forceinline__ uint32_t montu(uint32_t a_m, uint32_t x, const MontP& M) {
-    if constexpr (ASM) return red1(redc_su(mul_su(a_m, x), M), M.p);
-    else return red1(redc_lazy((uint64_t)a_m * x, M), M.p);
-}
-// (a' x + b' y) mod p in [0, p)   (a' x + b' y < 2 p^2 < p R)
-template <bool ASM>
-__device__ __forceinline__ uint32_t montu2(uint32_t a_m, uint32_t x, uint32_t b_m, uint32_t y, const MontP& M) {
-    if constexpr (ASM) return red1(redc_su(mad_su(b_m, y, mul_su(a_m, x)), M), M.p);
-    else return red1(redc_lazy((uint64_t)a_m * x + (uint64_t)b_m * y, M), M.p);
-}
-
 // radix-2 butterfly (u ± w c) % p.  The signs come from the exact i64 dividends (one
 // v_mad_i64_i32 each), the residues from one lazy Montgomery product shared by both outputs.
 

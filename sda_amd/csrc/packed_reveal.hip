@@ -72,7 +72,9 @@ __device__ __forceinline__ void reveal_flush(int64_t* lds_o, int64_t* o, uint64_
 
 // KU > 0: the evaluation loop over the k <= KU secrets is unrolled (table offsets become
 // compile-time constants: merged scalar loads, no per-secret loop overhead).
-template <int MMAX, bool STAGED, int KU>
+// LAZY (p >= kLazyTruncMinP): lazy truncation (packed_common.h: Trunc) with the -p trap; a lane
+// whose batch hit it recomputes the batch on the generic exact path.
+template <int MMAX, bool STAGED, int KU, bool LAZY>
 __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t* __restrict__ shares, uint64_t B,
                                                                   uint64_t D, int64_t* __restrict__ out,
                                                                   uint32_t n_idx, uint32_t k,
@@ -98,9 +100,8 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
     static_for<1, MMAX>([&](auto i) {
         in_range = in_range && ((uint32_t)i >= m || (uint64_t)(v[i] + (P - 1)) < (uint64_t)(2 * P - 1));
     });
-    if (!in_range) {
-        if (live) reveal_exact_generic(sh, B, m, k, tab, M, dst, lim);
-    } else {
+    Trunc<LAZY> tr;
+    if (in_range) {
         FE s[MMAX];
         s[0] = FE{0, 0};
         static_for<1, MMAX>([&](auto i) {
@@ -113,8 +114,9 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
         auto newton_step = [&](auto i, uint32_t j) {
             const uint32_t dc = s[i].c - s[i - 1].c + p;      // lazy: (0, 2p), REDC input < 2p^2 < pR
             const int32_t sg = __builtin_elementwise_sub_sat(s[i].s, s[i - 1].s);
-            const uint32_t fc = red1(redc_lazy((uint64_t)tab[OFF_INVM + j * TS + i] * dc, M), p);
-            s[i] = FE{trunc_rep(fc, (uint32_t)sg, p), fc};
+            const uint32_t fc = montu<LAZY>(tab[OFF_INVM + j * TS + i], dc, M);
+            s[i] = FE{tr(fc, (uint32_t)sg, p), fc};
+            tr.note1(s[i].s);
         };
         if constexpr (MMAX <= 16) {
             // fully unrolled triangle: every table word is a compile-time offset (merged s_loads)
@@ -135,6 +137,8 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
                 });
             }
         }
+        uint32_t sgm[MMAX];
+        static_for<0, MMAX>([&](auto i) { sgm[i] = (uint32_t)(s[i].s >> 31); });
         // numtheory::newton_evaluate at omega_secrets^(e+1): fold((a + (coef * np) % p) % p)
         auto eval = [&](uint32_t e) {
             const uint32_t* np = tab + OFF_NP + e * TS;
@@ -142,10 +146,16 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
             FE acc{0, 0};
             static_for<0, MMAX>([&](auto i) {
                 if ((uint32_t)i < m) {
-                    const uint32_t tc = red1(redc_lazy((uint64_t)npm[i] * s[i].c, M), p);
-                    const int32_t ts = trunc_rep(tc, (uint32_t)s[i].s ^ np[i], p);   // sign of s * np
+                    const uint32_t tc = montu<LAZY>(npm[i], s[i].c, M);
+                    // sign of s * np (np != 0 mod p; s == 0 makes tc == 0, exact unless LAZY, whose
+                    // trap then sends the batch to the generic path).  LAZY: p & (sgn(s) ^ sgn(np))
+                    // is one v_bitop3 with the per-coefficient sign masks hoisted out of the e loop.
+                    int32_t ts;
+                    if constexpr (LAZY) ts = (int32_t)(tc - (p & (sgm[i] ^ (uint32_t)((int32_t)np[i] >> 31))));
+                    else ts = tr(tc, (uint32_t)s[i].s ^ np[i], p);
                     const uint32_t ac = addm(acc.c, tc, p);
-                    acc = FE{trunc_rep(ac, (uint32_t)__builtin_elementwise_add_sat(acc.s, ts), p), ac};
+                    acc = FE{tr(ac, (uint32_t)__builtin_elementwise_add_sat(acc.s, ts), p), ac};
+                    tr.note2(ts, acc.s);
                 }
             });
             if (e < lim) dst[e] = acc.s;                                                // batched.rs:94
@@ -155,6 +165,9 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
         } else {
             for (uint32_t e = 0; e < k; ++e) eval(e);
         }
+    }
+    if (!in_range || tr.bad(p)) {
+        if (live) reveal_exact_generic(sh, B, m, k, tab, M, dst, lim);
     }
     reveal_flush<STAGED>(lds_o, o, b0, B, D, k);
 }
@@ -216,15 +229,18 @@ hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32
     const bool staged = k <= 16;                      // LDS stage: 256 * k * 8 B <= 32 KiB
     const size_t lds = staged ? (size_t)256 * k * sizeof(int64_t) : 0;
     if (mode == 0) {
-        if (staged && k <= 8 && MM <= 16)
-            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8>), grid, dim3(256), lds, s, a.shares, B,
-                               a.dimension, a.out, n_idx, k, tab, M);
+        if (staged && k <= 8 && MM <= 16 && M.p >= kLazyTruncMinP)
+            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, true>), grid, dim3(256), lds, s, a.shares,
+                               B, a.dimension, a.out, n_idx, k, tab, M);
+        else if (staged && k <= 8 && MM <= 16)
+            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, false>), grid, dim3(256), lds, s, a.shares,
+                               B, a.dimension, a.out, n_idx, k, tab, M);
         else if (staged)
-            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 0>), grid, dim3(256), lds, s, a.shares, B,
-                               a.dimension, a.out, n_idx, k, tab, M);
+            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 0, false>), grid, dim3(256), lds, s, a.shares,
+                               B, a.dimension, a.out, n_idx, k, tab, M);
         else
-            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, false, 0>), grid, dim3(256), 0, s, a.shares, B,
-                               a.dimension, a.out, n_idx, k, tab, M);
+            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, false, 0, false>), grid, dim3(256), 0, s, a.shares,
+                               B, a.dimension, a.out, n_idx, k, tab, M);
     } else {
         if (staged)
             hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, true>), grid, dim3(256), lds, s, a.shares, B,

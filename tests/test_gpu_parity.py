@@ -376,3 +376,32 @@ def test_packed_generate_negative_multiple_of_p(engine, oracle, sch):
             put(bb, c, (p - a) if bb % 2 else -(p - a))     # u - c == -p   /   u + c == -p
     got = engine.share_generate(sch, secrets, draws)
     assert_same(got, oracle.packed_generate(_pp(oracle, sch), secrets, draws))
+
+
+@pytest.mark.parametrize("sch", [s for s in packed_schemes() if s.prime_modulus >= 2**24 and
+                                 s.secret_count <= 8 and s.reconstruction_threshold() <= 15],
+                         ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")
+def test_packed_reconstruct_traps(engine, oracle, sch):
+    """Exact reveal where a Newton difference is exactly -p, or a coefficient is 0 (all-zero
+    shares): the lazily truncating kernel (p >= 2^24, k <= 8, <= 16 points) must fall back to the
+    generic exact path for those batches only."""
+    p, n = sch.prime_modulus, sch.share_count
+    rng = np.random.default_rng(p % 3001 + n)
+    k = sch.secret_count
+    B = 150
+    D = B * k - (1 if k > 1 else 0)               # ragged tail batch where k allows it
+    need = sch.reconstruction_threshold()
+    for size in sorted({need, min(n, 15)}):
+        idx = rng.permutation(n)[:size].tolist()
+        sh = rng.integers(-(p - 1), p, size=(size, B), dtype=np.int64)
+        for b in range(0, B, 2):                  # share[r] - share[r-1] == -p (first Newton level)
+            if size >= 2:
+                r = int(rng.integers(1, size))
+                a = int(rng.integers(1, p))
+                sh[r, b], sh[r - 1, b] = -a, p - a
+        sh[:, 3] = 0                              # zero Newton coefficients
+        sh[:, 7] = 0
+        got = engine.secret_reconstruct(sch, D, [(i, sh[j]) for j, i in enumerate(idx)])
+        rc, exp = oracle.packed_reconstruct(_pp(oracle, sch), D, idx, sh)
+        assert rc == 0
+        assert_same(got, exp)
