@@ -64,6 +64,10 @@ constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
 #ifndef SDA_GEN_WAVES
 #define SDA_GEN_WAVES 4
 #endif
+// Waves per EU: 5 where the transform fits 102 VGPRs without spilling (canonical and lazy-exact at
+// L <= 16), else SDA_GEN_WAVES (4: 128 VGPRs).
+template <int L, bool CANON, bool LAZY>
+constexpr int gen_waves() { return (L <= 16 && (CANON || LAZY)) ? 5 : SDA_GEN_WAVES; }
 
 
 // CANONICAL share generation: the same transform in canonical residues [0, p) only -- no sign
@@ -140,7 +144,8 @@ __device__ __forceinline__ void transform_canon(const int64_t (&raw)[L], const G
 // (A persistent grid-stride variant was measured slower: the loop made hipcc keep the twiddle
 // words in SGPRs across tiles and spill.)
 template <int L, int N3, bool WIDE, bool CANON, bool LAZY>
-__global__ __launch_bounds__(gen_block<L>()) __attribute__((amdgpu_waves_per_eu(SDA_GEN_WAVES, SDA_GEN_WAVES)))
+__global__ __launch_bounds__(gen_block<L>())
+__attribute__((amdgpu_waves_per_eu(gen_waves<L, CANON, LAZY>(), gen_waves<L, CANON, LAZY>())))
 void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const int64_t* __restrict__ draws,
                        int64_t* __restrict__ out, uint32_t k, uint32_t t, uint64_t B,
                        const GenTables* __restrict__ Tp, unsigned int* __restrict__ log) {
@@ -158,8 +163,10 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
     const int64_t P = (int64_t)p;
     // LDS word e (batch-major [batch][k] secrets, then [batch][t] draws) lives at lpos(e): one pad
     // word per 16 keeps the even/odd lane->batch reads below 2-way bank conflicted (b64 optimum).
-    __shared__ int64_t lds[BS * (L - 1) + BS * (L - 1) / 16 + 1];
-    auto lpos = [](uint32_t e) { return e + (e >> 4); };
+    // (Unpadded at 5 waves/EU: 5 tiles of <= 31.75 KiB fit the 160 KiB LDS; the pad measured neutral.)
+    constexpr bool PAD = gen_waves<L, CANON, LAZY>() < 5;
+    __shared__ int64_t lds[BS * (L - 1) + (PAD ? BS * (L - 1) / 16 + 1 : 0)];
+    auto lpos = [](uint32_t e) { return PAD ? e + (e >> 4) : e; };
 
     {
         const GenTables& T = *Tp;
