@@ -29,7 +29,24 @@ __global__ __launch_bounds__(256) void ubench(uint32_t seed, uint64_t* sink) {
         if constexpr (OP == 9) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a##i) : "v"(b));            \
         if constexpr (OP == 10) asm volatile("v_perm_b32 %0, %0, %0, %1" : "+v"(a##i) : "v"(b));      \
         if constexpr (OP == 11) asm volatile("v_alignbit_b32 %0, %0, %0, 16" : "+v"(a##i));             \
-        if constexpr (OP == 12) asm volatile("v_xad_u32 %0, %0, %1, %0" : "+v"(a##i) : "v"(b));
+        if constexpr (OP == 12) asm volatile("v_xad_u32 %0, %0, %1, %0" : "+v"(a##i) : "v"(b)); \
+        if constexpr (OP == 13) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(a##i) : "v"(b));            \
+        if constexpr (OP == 14) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a##i) : "v"(b));            \
+        if constexpr (OP == 15) asm volatile("v_ashrrev_i32 %0, 3, %0" : "+v"(a##i));                   \
+        if constexpr (OP == 16) asm volatile("v_max_u32 %0, %0, %1" : "+v"(a##i) : "v"(b));            \
+        if constexpr (OP == 17) asm volatile("v_min3_u32 %0, %0, %1, %0" : "+v"(a##i) : "v"(b));       \
+        if constexpr (OP == 18) asm volatile("v_med3_u32 %0, %0, %1, %0" : "+v"(a##i) : "v"(b));       \
+        if constexpr (OP == 19) asm volatile("v_pk_add_u16 %0, %0, 0 op_sel:[1,0] op_sel_hi:[0,1]" : "+v"(a##i)); \
+        if constexpr (OP == 20) asm volatile("v_bitop3_b32 %0, %0, %1, %0 bitop3:0x6c" : "+v"(a##i) : "v"(b)); \
+        if constexpr (OP == 21) asm volatile("v_add3_u32 %0, %0, %1, %0" : "+v"(a##i) : "v"(b));       \
+        if constexpr (OP == 22) asm volatile("v_sub_i32 %0, %0, %1 clamp" : "+v"(a##i) : "v"(b));      \
+        if constexpr (OP == 23) asm volatile("v_bfi_b32 %0, %0, %1, %0" : "+v"(a##i) : "v"(b));        \
+        if constexpr (OP == 24) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[40:41]" : "+v"(a##i) : "v"(b) : "s40", "s41"); \
+        if constexpr (OP == 25) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(a##i) : "v"(b));     \
+        if constexpr (OP == 26) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a##i) : "v"(b));        \
+        if constexpr (OP == 27) asm volatile("v_add_co_u32 %0, vcc, %0, %1\n\tv_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(a##i) : "v"(b) : "vcc"); \
+        if constexpr (OP == 28) asm volatile("v_min_i32 %0, %0, %1" : "+v"(a##i) : "v"(b));            \
+        if constexpr (OP == 29) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a##i));
         REP8(STEP)
     }
     uint64_t s = (uint64_t)a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + w0 + w1 + w2 + w3 + w4 + w5 + w6 + w7;
@@ -69,6 +86,23 @@ int main() {
     run<10>("v_perm_b32", sink, 1);
     run<11>("v_alignbit_b32 (16)", sink, 1);
     run<12>("v_xad_u32", sink, 1);
+    run<13>("v_sub_u32", sink, 1);
+    run<14>("v_and_b32", sink, 1);
+    run<15>("v_ashrrev_i32", sink, 1);
+    run<29>("v_lshrrev_b32", sink, 1);
+    run<16>("v_max_u32", sink, 1);
+    run<28>("v_min_i32", sink, 1);
+    run<17>("v_min3_u32", sink, 1);
+    run<18>("v_med3_u32", sink, 1);
+    run<19>("v_pk_add_u16 (swap)", sink, 1);
+    run<20>("v_bitop3_b32", sink, 1);
+    run<21>("v_add3_u32", sink, 1);
+    run<22>("v_sub_i32 clamp", sink, 1);
+    run<23>("v_bfi_b32", sink, 1);
+    run<24>("v_cndmask_b32 (sgpr)", sink, 1);
+    run<25>("v_lshl_or_b32", sink, 1);
+    run<26>("v_mul_u32_u24", sink, 1);
+    run<27>("v_add_co + v_addc_co", sink, 2);
     run<0>("v_add_u32 (again)", sink, 1);
     (void)hipFree(sink);
     return 0;
