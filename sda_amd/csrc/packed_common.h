@@ -121,22 +121,35 @@ inline GenTables make_gen_tables(uint32_t L, uint32_t N3, int64_t p, int64_t ws,
 //   values, as opaque asm so the compiler cannot reassociate the chain and stretch live ranges);
 //   the batch is then recomputed by the generic exact path (share-gen: logged for the fix-up
 //   kernel; reveal: the lane's generic branch).  LAZY is launched only for p >= kLazyTruncMinP.
+#ifndef SDA_TRAP_ASM
+#define SDA_TRAP_ASM 1
+#endif
 template <bool LAZY>
 struct Trunc {
     int32_t smin = 0x7FFFFFFF;
     __device__ __forceinline__ int32_t operator()(uint32_t c, uint32_t sw, uint32_t p) {
         if constexpr (LAZY) {
-            int32_t s = (int32_t)(c - (p & (uint32_t)((int32_t)sw >> 31)));
-            asm("" : "+v"(s));        // opaque: keeps isel from widening the residue chain
-            return s;
+            return (int32_t)(c - (p & (uint32_t)((int32_t)sw >> 31)));
         }
         else return trunc_rep(c, sw, p);
     }
     __device__ __forceinline__ void note1(int32_t a) {
-        if constexpr (LAZY) asm("v_min_i32 %0, %0, %1" : "+v"(smin) : "v"(a));
+        if constexpr (LAZY) {
+#if SDA_TRAP_ASM
+            asm("v_min_i32 %0, %0, %1" : "+v"(smin) : "v"(a));
+#else
+            smin = min(smin, a);
+#endif
+        }
     }
     __device__ __forceinline__ void note2(int32_t a, int32_t b) {
-        if constexpr (LAZY) asm("v_min3_i32 %0, %0, %1, %2" : "+v"(smin) : "v"(a), "v"(b));
+        if constexpr (LAZY) {
+#if SDA_TRAP_ASM
+            asm("v_min3_i32 %0, %0, %1, %2" : "+v"(smin) : "v"(a), "v"(b));
+#else
+            smin = min(smin, min(a, b));
+#endif
+        }
     }
     static constexpr bool lazy = LAZY;
     __device__ __forceinline__ bool bad(uint32_t p) const { return LAZY && smin == -(int32_t)p; }

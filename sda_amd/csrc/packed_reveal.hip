@@ -74,7 +74,9 @@ __device__ __forceinline__ void reveal_flush(int64_t* lds_o, int64_t* o, uint64_
 // compile-time constants: merged scalar loads, no per-secret loop overhead).
 // LAZY (p >= kLazyTruncMinP): lazy truncation (packed_common.h: Trunc) with the -p trap; a lane
 // whose batch hit it recomputes the batch on the generic exact path.
-template <int MMAX, bool STAGED, int KU, bool LAZY>
+// FULL: the point count is exactly MMAX (n_idx + 1 == MMAX), so every `i < m` guard is a compile-time
+// constant: no per-step uniform branches, and the table rows load as merged s_load_dwordx16.
+template <int MMAX, bool STAGED, int KU, bool LAZY, bool FULL = false>
 __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t* __restrict__ shares, uint64_t B,
                                                                   uint64_t D, int64_t* __restrict__ out,
                                                                   uint32_t n_idx, uint32_t k,
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
     int64_t* o = out + vec * D;
     const uint32_t p = M.p;
     const int64_t P = (int64_t)p;
-    const uint32_t m = n_idx + 1;
+    const uint32_t m = FULL ? (uint32_t)MMAX : n_idx + 1;
     int64_t* dst = STAGED ? lds_o + tid * k : o + b * k;
     const uint32_t lim = STAGED ? k : (b * k < D ? (uint32_t)(D - b * k < k ? D - b * k : k) : 0u);
 
@@ -114,7 +116,7 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
         auto newton_step = [&](auto i, uint32_t j) {
             const uint32_t dc = s[i].c - s[i - 1].c + p;      // lazy: (0, 2p), REDC input < 2p^2 < pR
             const int32_t sg = __builtin_elementwise_sub_sat(s[i].s, s[i - 1].s);
-            const uint32_t fc = montu<LAZY>(tab[OFF_INVM + j * TS + i], dc, M);
+            const uint32_t fc = montu<false>(tab[OFF_INVM + j * TS + i], dc, M);
             s[i] = FE{tr(fc, (uint32_t)sg, p), fc};
             tr.note1(s[i].s);
         };
@@ -146,7 +148,7 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
             FE acc{0, 0};
             static_for<0, MMAX>([&](auto i) {
                 if ((uint32_t)i < m) {
-                    const uint32_t tc = montu<LAZY>(npm[i], s[i].c, M);
+                    const uint32_t tc = montu<false>(npm[i], s[i].c, M);
                     // sign of s * np (np != 0 mod p; s == 0 makes tc == 0, exact unless LAZY, whose
                     // trap then sends the batch to the generic path).  LAZY: p & (sgn(s) ^ sgn(np))
                     // is one v_bitop3 with the per-coefficient sign masks hoisted out of the e loop.
@@ -229,7 +231,10 @@ hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32
     const bool staged = k <= 16;                      // LDS stage: 256 * k * 8 B <= 32 KiB
     const size_t lds = staged ? (size_t)256 * k * sizeof(int64_t) : 0;
     if (mode == 0) {
-        if (staged && k <= 8 && MM <= 16 && M.p >= kLazyTruncMinP)
+        if (staged && k <= 8 && MM <= 16 && M.p >= kLazyTruncMinP && n_idx + 1 == MM)
+            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, true, true>), grid, dim3(256), lds, s,
+                               a.shares, B, a.dimension, a.out, n_idx, k, tab, M);
+        else if (staged && k <= 8 && MM <= 16 && M.p >= kLazyTruncMinP)
             hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, true>), grid, dim3(256), lds, s, a.shares,
                                B, a.dimension, a.out, n_idx, k, tab, M);
         else if (staged && k <= 8 && MM <= 16)
