@@ -57,6 +57,23 @@ struct Zero3 {
     }
 };
 
+// Streaming policy of the tile loads / share stores (A/B knobs; default: non-temporal both ways).
+#ifndef SDA_GEN_NT_LOAD
+#define SDA_GEN_NT_LOAD 1
+#endif
+#ifndef SDA_GEN_NT_STORE
+#define SDA_GEN_NT_STORE 1
+#endif
+__device__ __forceinline__ int64_t gen_load(const int64_t* a) {
+    if constexpr (SDA_GEN_NT_LOAD) return __builtin_nontemporal_load(a);
+    else return *a;
+}
+template <class V>
+__device__ __forceinline__ void gen_store(const V& v, V* a) {
+    if constexpr (SDA_GEN_NT_STORE) __builtin_nontemporal_store(v, a);
+    else *a = v;
+}
+
 // Workgroup size: 256 batches, fewer for the wide transforms so the LDS stage stays <= 32 KiB.
 template <int L>
 constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
@@ -188,7 +205,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                 int64_t v[U];
                 static_for<0, U>([&](auto u) {
                     const uint32_t e = base + u * BS + tid;
-                    v[u] = __builtin_nontemporal_load(ssrc + (e < valid ? e : 0));   // read once
+                    v[u] = gen_load(ssrc + (e < valid ? e : 0));   // read once
                 });
                 static_for<0, U>([&](auto u) {
                     const uint32_t e = base + u * BS + tid;
@@ -202,7 +219,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                 int64_t v[U];
                 static_for<0, U>([&](auto u) {
                     const uint32_t e = base + u * BS + tid;
-                    v[u] = __builtin_nontemporal_load(dsrc + (e < nd ? e : 0));
+                    v[u] = gen_load(dsrc + (e < nd ? e : 0));
                 });
                 static_for<0, U>([&](auto u) {
                     const uint32_t e = base + u * BS + tid;
@@ -356,7 +373,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                     typedef int32_t v4i __attribute__((ext_vector_type(4)));
                     v4i* d4 = reinterpret_cast<v4i*>(orow + (uint64_t)(2 * q) * B);
                     const v4i val = {lo, lo >> 31, hi, hi >> 31};
-                    __builtin_nontemporal_store(val, d4);       // streamed once: keep it out of L2/MALL
+                    gen_store(val, d4);       // streamed once: keep it out of L2/MALL
                 }
             });
         } else {                           // odd B: each lane stores its own batch
