@@ -237,6 +237,23 @@ sda_status sda_varint_encode_dev(sda_engine* h, const int64_t* vals, uint64_t ro
                                  uint64_t stride, uint8_t* dst, uint64_t dst_cap,
                                  uint64_t* row_bytes, void* stream);
 
+/* ---------------- snapshot transposition ----------------
+ * Replaces AggregationsStore::iter_snapshot_clerk_jobs_data (server/src/stores.rs:86-101; the Mongo
+ * store's $unwind/$group at server-store-mongodb/src/aggregations.rs:164-195): the snapshot's
+ * participations [participation][clerk] regrouped as clerking jobs [clerk][participation], each
+ * clerk's blobs in snapshot order.  Blobs are opaque bytes (sealed boxes or opened payloads).
+ *   src (device, 16-byte aligned, readable 32 bytes past part_off[P*n]): participation p's payload
+ *     for clerk c = src[part_off[p*n + c], part_off[p*n + c + 1]); part_off is a HOST array [P*n + 1].
+ *   dst (device, 16-byte aligned): clerk c's job starts at dst + clerk_base[c] (16-byte aligned) and
+ *     its blob p = [clerk_off[c*(P+1) + p], clerk_off[c*(P+1) + p + 1]) relative to that start, followed
+ *     by >= 16 readable bytes -- exactly the (bytes, blob_off) pair sda_clerk_decode_combine_dev takes.
+ *   clerk_base [n], clerk_off [n][P+1] (HOST, written); *dst_len = bytes of dst used.
+ *   dst == NULL: sizing query (offsets and *dst_len only, nothing launched). */
+sda_status sda_snapshot_transpose_dev(sda_engine* h, const uint8_t* src, const uint64_t* part_off,
+                                      uint64_t n_participations, uint64_t n_clerks, uint8_t* dst,
+                                      uint64_t dst_cap, uint64_t* dst_len, uint64_t* clerk_base,
+                                      uint64_t* clerk_off, void* stream);
+
 /* ---------------- fused role pipelines ---------------- */
 
 /* Recipient reveal (receive.rs:80-157) + RecipientOutput::positive (:14-20) as one device

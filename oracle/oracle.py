@@ -67,6 +67,8 @@ def lib():
         L.or_varint_encode.argtypes = [_i64p, C.c_size_t, C.POINTER(C.c_uint8)]
         L.or_varint_decode.restype = C.c_size_t
         L.or_varint_decode.argtypes = [C.POINTER(C.c_uint8), C.c_size_t, _i64p, C.c_size_t]
+        L.or_snapshot_transpose.argtypes = [C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.c_size_t, C.c_size_t,
+                                            C.POINTER(C.c_uint8), C.POINTER(C.c_uint64)]
         _lib = L
     return _lib
 
@@ -221,3 +223,20 @@ def varint_decode(data: bytes) -> np.ndarray:
     out, op = _i64(np.zeros(max(1, len(data)), np.int64))
     n = lib().or_varint_decode(src, len(data), op, out.size)
     return out[:n]
+
+
+def snapshot_transpose(blobs):
+    """server/src/stores.rs:86-101 iter_snapshot_clerk_jobs_data: blobs[p][c] (bytes) ->
+    per clerk the list of its blobs in snapshot order (restated in C: or_snapshot_transpose)."""
+    P = len(blobs)
+    n = len(blobs[0]) if P else 0
+    flat = b"".join(b for row in blobs for b in row)
+    off = np.concatenate([[0], np.cumsum([len(b) for row in blobs for b in row])]).astype(np.uint64)
+    src = (C.c_uint8 * max(1, len(flat))).from_buffer_copy(flat or b"\0")
+    out = (C.c_uint8 * max(1, len(flat)))()
+    coff = np.zeros(max(1, n * (P + 1)), np.uint64)
+    lib().or_snapshot_transpose(src, off.ctypes.data_as(C.POINTER(C.c_uint64)), P, n, out,
+                                coff.ctypes.data_as(C.POINTER(C.c_uint64)))
+    data = bytes(out[:len(flat)])
+    coff = coff[:n * (P + 1)].reshape(n, P + 1)
+    return [[data[coff[c, p]:coff[c, p + 1]] for p in range(P)] for c in range(n)]

@@ -411,3 +411,17 @@ size_t or_varint_decode(const uint8_t* in, size_t n_bytes, int64_t* out, size_t 
     }
     return c;
 }
+
+/* server/src/stores.rs:86-101: shares[ix].push(share) for every participation in snapshot order. */
+void or_snapshot_transpose(const uint8_t* in, const uint64_t* part_off, size_t P, size_t n,
+                           uint8_t* out, uint64_t* clerk_off) {
+    uint64_t w = 0;
+    for (size_t c = 0; c < n; ++c)
+        for (size_t p = 0; p <= P; ++p) {
+            clerk_off[c * (P + 1) + p] = w;
+            if (p == P) break;
+            const uint64_t b = part_off[p * n + c], e = part_off[p * n + c + 1];
+            memcpy(out + w, in + b, e - b);
+            w += e - b;
+        }
+}

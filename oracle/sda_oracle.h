@@ -108,6 +108,12 @@ void or_positive(int64_t m, const int64_t* vals, size_t D, int64_t* out);
 size_t or_varint_encode(const int64_t* vals, size_t n, uint8_t* out);
 size_t or_varint_decode(const uint8_t* in, size_t n_bytes, int64_t* out, size_t cap);
 
+/* server/src/stores.rs:86-101 iter_snapshot_clerk_jobs_data: [participation][clerk] blobs regrouped
+ * per clerk in snapshot order.  in blob (p, c) = in[part_off[p*n+c], part_off[p*n+c+1]); out gets
+ * clerk 0's blobs back to back, then clerk 1's, ...; clerk_off [n][P+1] absolute offsets into out. */
+void or_snapshot_transpose(const uint8_t* in, const uint64_t* part_off, size_t P, size_t n,
+                           uint8_t* out, uint64_t* clerk_off);
+
 #ifdef __cplusplus
 }
 #endif

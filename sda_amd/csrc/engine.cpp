@@ -34,6 +34,8 @@ struct sda_engine {
     void* pipe = nullptr;         // recipient / participant pipeline scratch (mask, masked, compacted shares)
     size_t pipe_bytes = 0;
     sda::DeviceTable rev_tab;     // packed-Shamir Newton/Lagrange tables (per scheme + clerk set)
+    void* snap = nullptr;         // snapshot transposition copy plan
+    size_t snap_bytes = 0;
 };
 
 namespace {
@@ -205,6 +207,7 @@ void sda_engine_destroy(sda_engine* h) {
     if (h->codec_work) (void)hipFree(h->codec_work);
     if (h->codec_mat) (void)hipFree(h->codec_mat);
     if (h->pipe) (void)hipFree(h->pipe);
+    if (h->snap) (void)hipFree(h->snap);
     if (h->stage) (void)hipFree(h->stage);
     sda::free_table(h->gen_tab);
     sda::free_table(h->rev_tab);
@@ -805,6 +808,66 @@ sda_status sda_varint_encode_dev(sda_engine* h, const int64_t* vals, uint64_t ro
                                              pick(h, stream));
     if (e == hipErrorInvalidValue) return fail(SDA_ERR_INVALID_ARGUMENT, "dst_cap too small");
     HIP_TRY(e);
+    return ok();
+}
+
+// ---------------- snapshot transposition (stores.rs:86-101) ----------------
+// Offsets are a host-side plan (like the codec's blob_off); the bytes move on the device.
+sda_status sda_snapshot_transpose_dev(sda_engine* h, const uint8_t* src, const uint64_t* part_off,
+                                      uint64_t n_participations, uint64_t n_clerks, uint8_t* dst, uint64_t dst_cap,
+                                      uint64_t* dst_len, uint64_t* clerk_base, uint64_t* clerk_off, void* stream) {
+    if (!h || !part_off || !dst_len || (n_clerks && (!clerk_base || !clerk_off)))
+        return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    const uint64_t P = n_participations, n = n_clerks, nb = P * n;
+    if (n && P > ((uint64_t)1 << 32) / n) return fail(SDA_ERR_UNSUPPORTED, "at most 2^32 blobs per snapshot");
+    for (uint64_t b = 0; b < nb; ++b)
+        if (part_off[b + 1] < part_off[b]) return fail(SDA_ERR_INVALID_ARGUMENT, "blob offsets must be non-decreasing");
+    // clerk c's job: its P blobs back to back in snapshot order, the job 16-byte aligned and followed
+    // by 16 readable bytes (what sda_clerk_decode_combine_dev takes)
+    uint64_t total = 0;
+    for (uint64_t c = 0; c < n; ++c) {
+        clerk_base[c] = total;
+        uint64_t* off = clerk_off + c * (P + 1);
+        off[0] = 0;
+        for (uint64_t p = 0; p < P; ++p) off[p + 1] = off[p] + (part_off[p * n + c + 1] - part_off[p * n + c]);
+        total += ((off[P] + 15) & ~(uint64_t)15) + 16;
+    }
+    *dst_len = total;
+    if (!dst) return ok();                                          // sizing query
+    if (dst_cap < total) return fail(SDA_ERR_INVALID_ARGUMENT, "dst_cap %llu < %llu bytes needed",
+                                     (unsigned long long)dst_cap, (unsigned long long)total);
+    if (nb && !src) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (((uintptr_t)src & 15) || ((uintptr_t)dst & 15))
+        return fail(SDA_ERR_INVALID_ARGUMENT, "src and dst must be 16-byte aligned");
+    const uint64_t chunk = sda::snapshot_chunk_bytes();
+    std::vector<sda::SnapshotCopy> blobs;
+    std::vector<uint32_t> bblob, bchunk;
+    blobs.reserve(nb);
+    for (uint64_t c = 0; c < n; ++c)
+        for (uint64_t p = 0; p < P; ++p) {
+            const uint64_t len = part_off[p * n + c + 1] - part_off[p * n + c];
+            if (!len) continue;
+            const uint32_t id = (uint32_t)blobs.size();
+            blobs.push_back({part_off[p * n + c], clerk_base[c] + clerk_off[c * (P + 1) + p], len});
+            for (uint64_t k = 0; k * chunk < len; ++k) {
+                bblob.push_back(id);
+                bchunk.push_back((uint32_t)k);
+            }
+        }
+    if (blobs.empty()) return ok();
+    if (bblob.size() > 0x7fffffffu) return fail(SDA_ERR_UNSUPPORTED, "snapshot too large for one launch");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = pick(h, stream);
+    const size_t b0 = rup(blobs.size() * sizeof(sda::SnapshotCopy)), b1 = rup(bblob.size() * 4);
+    if (sda_status e = ensure(&h->snap, &h->snap_bytes, b0 + 2 * b1)) return e;
+    char* plan = static_cast<char*>(h->snap);
+    HIP_TRY(hipMemcpyAsync(plan, blobs.data(), blobs.size() * sizeof(sda::SnapshotCopy), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(plan + b0, bblob.data(), bblob.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(plan + b0 + b1, bchunk.data(), bchunk.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(sda::launch_snapshot_transpose(src, dst, reinterpret_cast<const sda::SnapshotCopy*>(plan),
+                                           reinterpret_cast<const uint32_t*>(plan + b0),
+                                           reinterpret_cast<const uint32_t*>(plan + b0 + b1), bblob.size(), st));
+    HIP_TRY(hipStreamSynchronize(st));                             // the host plan vectors go out of scope
     return ok();
 }
 

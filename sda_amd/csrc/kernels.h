@@ -108,4 +108,16 @@ hipError_t launch_chacha_mask(int64_t modulus, const uint32_t* seed_host, uint32
                               const int64_t* secrets, uint64_t D, int64_t* masked, void* work,
                               hipStream_t s);
 
+// ---- snapshot.hip ----
+// One blob of the snapshot transposition: len bytes from src offset to dst offset.
+struct SnapshotCopy {
+    uint64_t src, dst, len;
+};
+uint64_t snapshot_chunk_bytes();
+// workgroup i moves chunk block_chunk[i] of blob block_blob[i]; src/dst 16-byte aligned,
+// src readable 16 bytes past the last blob's 16-rounded end.
+hipError_t launch_snapshot_transpose(const uint8_t* src, uint8_t* dst, const SnapshotCopy* blobs,
+                                     const uint32_t* block_blob, const uint32_t* block_chunk, uint64_t n_blocks,
+                                     hipStream_t s);
+
 }  // namespace sda

@@ -94,6 +94,8 @@ SIGNATURES = [
     ("sda_varint_decode_dev", _st, [_vp, _vp, _u64p, C.c_uint64, _vp, C.c_uint64, _u64p, _vp]),
     ("sda_clerk_decode_combine_dev", _st, [_vp, C.c_int64, _vp, _u64p, C.c_uint64, _vp, C.c_uint64, _u64p, _vp]),
     ("sda_varint_encode_dev", _st, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp, C.c_uint64, _u64p, _vp]),
+    ("sda_snapshot_transpose_dev", _st, [_vp, _vp, _u64p, C.c_uint64, C.c_uint64, _vp, C.c_uint64, _u64p, _u64p,
+                                         _u64p, _vp]),
     ("sda_recipient_reveal_dev", _st, [_vp, C.POINTER(S.MaskingSchemeC), _vp, C.c_uint64, C.c_uint64,
                                        C.POINTER(S.SharingSchemeC), C.c_uint64, _u64p, _vp, C.c_uint64, C.c_uint64,
                                        C.c_int64, C.c_int32, _vp, C.c_uint64, _u64p, _vp]),
@@ -353,6 +355,23 @@ class Engine:
         _check(self.lib.sda_varint_encode_dev(self.h, vals_ptr, rows, length, stride, dst_ptr, dst_cap,
                                               _ptr(rb, _u64p), stream))
         return rb[:rows]
+
+    def snapshot_transpose_dev(self, src_ptr, part_off, n_participations, n_clerks, dst_ptr=None, dst_cap=0,
+                               stream=None):
+        """AggregationsStore::iter_snapshot_clerk_jobs_data (server/src/stores.rs:86-101) on device.
+
+        part_off: [P*n + 1] offsets of the [participation][clerk] blobs in src.  Returns
+        (dst_len, clerk_base [n], clerk_off [n][P+1]); dst_ptr None = sizing query."""
+        off = _arr(part_off, np.uint64)
+        P, n = n_participations, n_clerks
+        if off.size != P * n + 1:
+            raise ValueError("part_off must have n_participations * n_clerks + 1 entries")
+        base = np.zeros(max(n, 1), np.uint64)
+        coff = np.zeros(max(n * (P + 1), 1), np.uint64)
+        dlen = C.c_uint64(0)
+        _check(self.lib.sda_snapshot_transpose_dev(self.h, src_ptr, _ptr(off, _u64p), P, n, dst_ptr, dst_cap,
+                                                   C.byref(dlen), _ptr(base, _u64p), _ptr(coff, _u64p), stream))
+        return dlen.value, base[:n], coff[:n * (P + 1)].reshape(n, P + 1)
 
     def recipient_reveal_dev(self, masking, mask_ptr, n_masks, mask_width, sharing, dimension, indices, shares_ptr,
                              share_len, output_modulus, out_ptr, out_cap, mode=REVEAL_EXACT, stream=None) -> int:

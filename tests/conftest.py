@@ -14,6 +14,11 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def engine():
+    # torch's HIP runtime must open the device before the engine's (ROCm) runtime does; with the
+    # opposite order torch reports "No HIP GPUs are available" in the same process
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
     from sda_amd import Engine
     e = Engine(0)
     yield e
