@@ -53,8 +53,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-check", action="store_true", help="A/B helper: skip the side-leg round-trip checks")
     ap.add_argument("--codec-rows", type=int, default=1000, help="participations in the codec leg")
+    ap.add_argument("--snapshot-participations", type=int, default=1000,
+                    help="participations in the snapshot transposition leg")
     ap.add_argument("--pipeline-dim", type=int, default=10_000_000, help="vector dimension of the role pipelines")
-    ap.add_argument("--only", choices=["combine", "shamir", "chacha", "codec", "pipelines"], default=None,
+    ap.add_argument("--only", choices=["combine", "shamir", "chacha", "codec", "snapshot", "pipelines"], default=None,
                     help="profile helper: run just one leg (no JSON contract)")
     return ap.parse_args()
 
@@ -316,6 +318,48 @@ def main():
         }
         log(f"[codec] {json.dumps(side['codec'])}")
         del x, buf, mat
+
+    if not args.no_side and args.only in (None, "snapshot"):
+        # server side (stores.rs:86-101): a snapshot of Ps participations x 26 clerk payloads of
+        # packed-Shamir 1M-dim shares (B = 125,000 varint shares, ~4.94 B each -> ~617 KB per payload,
+        # ragged) regrouped into 26 clerking jobs.  Algorithmic bytes = read + write of every payload.
+        Ps, ncl = args.snapshot_participations, 26
+        g = np.random.default_rng(SEED_BASE + 11)
+        lens = g.integers(600_000, 635_000, size=Ps * ncl)
+        poff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        total = int(poff[-1])
+        src = torch.empty(total + 32, dtype=torch.uint8, device=dev)
+        eng.synth_fill_dev(src.data_ptr(), 1, (total + 32) // 8, SEED_BASE + 11, -(2**61), 2**61, stream())
+        need, _, _ = eng.snapshot_transpose_dev(src.data_ptr(), poff, Ps, ncl)
+        dst = torch.empty(need, dtype=torch.uint8, device=dev)
+        stt = Timer(torch)
+        for i in range(2 + max(2, args.steps // 4)):
+            f = lambda: eng.snapshot_transpose_dev(src.data_ptr(), poff, Ps, ncl, dst.data_ptr(), need, stream())  # noqa
+            stt.record(f) if i >= 2 else f()
+        _, base, coff = eng.snapshot_transpose_dev(src.data_ptr(), poff, Ps, ncl, None, 0)
+        torch.cuda.synchronize()
+        if not args.no_check:
+            for c, pp in ((0, 0), (7, Ps // 3), (ncl - 1, Ps - 1), (13, Ps // 2)):
+                b = pp * ncl + c
+                lo = int(base[c] + coff[c, pp])
+                if not torch.equal(dst[lo:lo + int(lens[b])], src[int(poff[b]):int(poff[b + 1])]):
+                    raise SystemExit("snapshot transposition FAILED")
+        s_ms = stt.mean_ms()
+        cpt = Timer(torch)                               # same-size device-to-device copy: the copy ceiling
+        for i in range(4):
+            f = lambda: dst[:total].copy_(src[:total])  # noqa
+            cpt.record(f) if i else f()
+        cp_ms = cpt.mean_ms()
+        side["snapshot"] = {
+            "config": f"{Ps} participations x {ncl} clerk payloads of ~617 KB (ragged), {total / 1e9:.2f} GB",
+            "ms": s_ms, "payload_GBps": total / (s_ms * 1e-3) / 1e9,
+            "hbm_GBps": 2.0 * total / (s_ms * 1e-3) / 1e9,
+            "roofline_frac": 2.0 * total / (s_ms * 1e-3) / 8.0e12,
+            "d2d_copy_ms": cp_ms, "d2d_copy_hbm_GBps": 2.0 * total / (cp_ms * 1e-3) / 1e9,
+            "note": "call time (host plan of one entry per blob + upload + kernel), HIP events",
+        }
+        log(f"[snapshot] {json.dumps(side['snapshot'])}")
+        del src, dst
 
     if not args.no_side and args.only in (None, "pipelines"):
         # configs[4] per GPU: participant = ChaCha mask -> packed share-gen -> per-clerk payload encoding

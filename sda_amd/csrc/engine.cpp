@@ -840,33 +840,28 @@ sda_status sda_snapshot_transpose_dev(sda_engine* h, const uint8_t* src, const u
     if (((uintptr_t)src & 15) || ((uintptr_t)dst & 15))
         return fail(SDA_ERR_INVALID_ARGUMENT, "src and dst must be 16-byte aligned");
     const uint64_t chunk = sda::snapshot_chunk_bytes();
-    std::vector<sda::SnapshotCopy> blobs;
-    std::vector<uint32_t> bblob, bchunk;
+    std::vector<sda::SnapshotCopy> blobs;                          // clerk-major, non-empty blobs only
+    std::vector<uint64_t> cstart(1, 0);
     blobs.reserve(nb);
+    cstart.reserve(nb + 1);
     for (uint64_t c = 0; c < n; ++c)
         for (uint64_t p = 0; p < P; ++p) {
             const uint64_t len = part_off[p * n + c + 1] - part_off[p * n + c];
             if (!len) continue;
-            const uint32_t id = (uint32_t)blobs.size();
             blobs.push_back({part_off[p * n + c], clerk_base[c] + clerk_off[c * (P + 1) + p], len});
-            for (uint64_t k = 0; k * chunk < len; ++k) {
-                bblob.push_back(id);
-                bchunk.push_back((uint32_t)k);
-            }
+            cstart.push_back(cstart.back() + (len + chunk - 1) / chunk);
         }
     if (blobs.empty()) return ok();
-    if (bblob.size() > 0x7fffffffu) return fail(SDA_ERR_UNSUPPORTED, "snapshot too large for one launch");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = pick(h, stream);
-    const size_t b0 = rup(blobs.size() * sizeof(sda::SnapshotCopy)), b1 = rup(bblob.size() * 4);
-    if (sda_status e = ensure(&h->snap, &h->snap_bytes, b0 + 2 * b1)) return e;
+    const size_t b0 = rup(blobs.size() * sizeof(sda::SnapshotCopy));
+    if (sda_status e = ensure(&h->snap, &h->snap_bytes, b0 + rup(cstart.size() * 8))) return e;
     char* plan = static_cast<char*>(h->snap);
     HIP_TRY(hipMemcpyAsync(plan, blobs.data(), blobs.size() * sizeof(sda::SnapshotCopy), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(plan + b0, bblob.data(), bblob.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(plan + b0 + b1, bchunk.data(), bchunk.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(plan + b0, cstart.data(), cstart.size() * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(sda::launch_snapshot_transpose(src, dst, reinterpret_cast<const sda::SnapshotCopy*>(plan),
-                                           reinterpret_cast<const uint32_t*>(plan + b0),
-                                           reinterpret_cast<const uint32_t*>(plan + b0 + b1), bblob.size(), st));
+                                           reinterpret_cast<const uint64_t*>(plan + b0), blobs.size(),
+                                           cstart.back(), st));
     HIP_TRY(hipStreamSynchronize(st));                             // the host plan vectors go out of scope
     return ok();
 }

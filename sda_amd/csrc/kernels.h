@@ -114,10 +114,10 @@ struct SnapshotCopy {
     uint64_t src, dst, len;
 };
 uint64_t snapshot_chunk_bytes();
-// workgroup i moves chunk block_chunk[i] of blob block_blob[i]; src/dst 16-byte aligned,
-// src readable 16 bytes past the last blob's 16-rounded end.
+// blobs[n_blobs] (each len >= 1), chunk_start[n_blobs + 1] = exclusive prefix of ceil(len / chunk);
+// src/dst 16-byte aligned, src readable 32 bytes past the last blob's end.
 hipError_t launch_snapshot_transpose(const uint8_t* src, uint8_t* dst, const SnapshotCopy* blobs,
-                                     const uint32_t* block_blob, const uint32_t* block_chunk, uint64_t n_blocks,
+                                     const uint64_t* chunk_start, uint64_t n_blobs, uint64_t total_chunks,
                                      hipStream_t s);
 
 }  // namespace sda

@@ -8,11 +8,14 @@
 // ([participation][clerk] ragged byte blobs); the clerking jobs want [clerk][participation].
 // This is a ragged byte gather: HBM-bound, 2 bytes of traffic per payload byte.
 //
-// One workgroup moves one 16 KiB chunk of one blob.  Every lane owns 16-byte aligned DESTINATION
-// quads so stores are dwordx4; the source shift (src - dst) mod 16 is the same for the whole blob,
-// so the byte re-alignment is a wave-uniform switch over v_alignbyte on two dwordx4 loads (the
-// second one is the neighbouring lane's first, served from the TCP).  The <16-byte head and tail
-// of the chunk, where a quad is shared with the adjacent blob, are written with byte stores.
+// Blobs are cut into 32 KiB chunks; a workgroup moves a contiguous run of them.  Every lane owns
+// 16-byte aligned DESTINATION quads so stores are dwordx4.  The source shift (src - dst) mod 16 is
+// uniform per blob: shift 0 takes aligned dwordx4 loads; any other shift takes one unaligned dwordx4
+// load per quad (gfx950 runs with unaligned access mode, so the hardware splits the line crossing).
+// A/B (profiles/r01h/ab_snapshot.txt): unaligned 7.25 ms vs 7.57 ms for two aligned loads + a
+// uniform switch over v_alignbyte (SDA_SNAP_UNALIGNED=0), 91% of a same-size device-to-device copy.
+// All loads of a chunk are issued before its stores.  The <16-byte head and tail of a chunk, whose
+// quad is shared with the neighbouring blob, are written with byte stores.
 #include "kernels.h"
 
 namespace sda {
@@ -20,8 +23,14 @@ namespace sda {
 namespace {
 
 constexpr uint32_t kThreads = 256;
-constexpr uint32_t kQuadsPerThread = 4;
-constexpr uint64_t kChunk = (uint64_t)kThreads * kQuadsPerThread * 16;   // 16 KiB per workgroup
+#ifndef SDA_SNAP_UNALIGNED
+#define SDA_SNAP_UNALIGNED 1
+#endif
+#ifndef SDA_SNAP_QUADS
+#define SDA_SNAP_QUADS 8
+#endif
+constexpr uint32_t kQuadsPerThread = SDA_SNAP_QUADS;
+constexpr uint64_t kChunk = (uint64_t)kThreads * kQuadsPerThread * 16;   // 32 KiB per workgroup
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -44,31 +53,34 @@ __device__ __forceinline__ u32x4 window(const u32x4& a, const u32x4& b) {
 template <int O>
 __device__ __forceinline__ void copy_body(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                           uint64_t d_lo, uint64_t d_hi, int64_t shift) {
-    // dst quads [d_lo, d_hi) (16-aligned absolute dst offsets); source byte = dst byte + shift
+    // dst quads [d_lo, d_hi) (16-aligned absolute dst offsets); source byte = dst byte + shift.
+    // All loads of the chunk are issued before the first store (kQuadsPerThread x 32 B in flight per lane).
+    u32x4 v[kQuadsPerThread];
+#pragma unroll
     for (uint32_t it = 0; it < kQuadsPerThread; ++it) {
         const uint64_t d = d_lo + ((uint64_t)it * kThreads + threadIdx.x) * 16;
-        if (d >= d_hi) break;
-        const uint64_t s = (uint64_t)((int64_t)d + shift);
-        const u32x4* p = reinterpret_cast<const u32x4*>(src + (s & ~(uint64_t)15));
-        const u32x4 a = p[0];
-        u32x4 v;
-        if constexpr (O == 0) {
-            v = a;
-        } else {
-            const u32x4 b = p[1];
-            v = window<O / 4, O % 4>(a, b);
+        if (d < d_hi) {
+            const uint64_t s = (uint64_t)((int64_t)d + shift);
+            const u32x4* p = reinterpret_cast<const u32x4*>(src + (s & ~(uint64_t)15));
+            if constexpr (O == 0) {
+                v[it] = p[0];
+            } else if constexpr (SDA_SNAP_UNALIGNED) {
+                __builtin_memcpy(&v[it], src + s, 16);     // one unaligned dwordx4 (unaligned access mode)
+            } else {
+                v[it] = window<O / 4, O % 4>(p[0], p[1]);
+            }
         }
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + d));
+    }
+#pragma unroll
+    for (uint32_t it = 0; it < kQuadsPerThread; ++it) {
+        const uint64_t d = d_lo + ((uint64_t)it * kThreads + threadIdx.x) * 16;
+        if (d < d_hi) __builtin_nontemporal_store(v[it], reinterpret_cast<u32x4*>(dst + d));
     }
 }
 
-__global__ __launch_bounds__(kThreads) void snapshot_transpose_kernel(const uint8_t* __restrict__ src,
-                                                                      uint8_t* __restrict__ dst,
-                                                                      const SnapshotCopy* __restrict__ blobs,
-                                                                      const uint32_t* __restrict__ block_blob,
-                                                                      const uint32_t* __restrict__ block_chunk) {
-    const SnapshotCopy c = blobs[block_blob[blockIdx.x]];
-    const uint64_t c0 = (uint64_t)block_chunk[blockIdx.x] * kChunk;
+__device__ __forceinline__ void copy_chunk(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                           const SnapshotCopy& c, uint64_t chunk) {
+    const uint64_t c0 = chunk * kChunk;
     const uint64_t c1 = c0 + kChunk < c.len ? c0 + kChunk : c.len;
     const uint64_t a = c.dst + c0, e = c.dst + c1;            // absolute dst byte range of this chunk
     const int64_t shift = (int64_t)c.src - (int64_t)c.dst;
@@ -77,8 +89,7 @@ __global__ __launch_bounds__(kThreads) void snapshot_transpose_kernel(const uint
     // head [a, A) and tail [E, e): < 16 bytes each, byte stores (quads shared with neighbouring blobs)
     const uint32_t t = threadIdx.x;
     if (t < 16 && a + t < A) dst[a + t] = src[(uint64_t)((int64_t)(a + t) + shift)];
-    if (t >= 32 && t < 48 && E + (t - 32) < e && E + (t - 32) >= A)
-        dst[E + (t - 32)] = src[(uint64_t)((int64_t)(E + (t - 32)) + shift)];
+    if (t >= 64 && t < 80 && E + (t - 64) < e) dst[E + (t - 64)] = src[(uint64_t)((int64_t)(E + (t - 64)) + shift)];
     if (A >= E) return;
     switch ((uint32_t)((uint64_t)shift & 15)) {               // uniform over the workgroup
 #define SDA_CASE(O) case O: copy_body<O>(src, dst, A, E, shift); break;
@@ -88,23 +99,47 @@ __global__ __launch_bounds__(kThreads) void snapshot_transpose_kernel(const uint
     }
 }
 
+// Workgroup w walks the contiguous chunk range [total*w/G, total*(w+1)/G) of the clerk-major blob
+// list: one binary search over the chunk prefix for its first blob, then a forward walk, so the
+// host plan is one entry per blob and a workgroup never waits on per-chunk table lookups.
+__global__ __launch_bounds__(kThreads) void snapshot_transpose_kernel(const uint8_t* __restrict__ src,
+                                                                      uint8_t* __restrict__ dst,
+                                                                      const SnapshotCopy* __restrict__ blobs,
+                                                                      const uint64_t* __restrict__ chunk_start,
+                                                                      uint64_t n_blobs, uint64_t total_chunks) {
+    const uint64_t G = gridDim.x, w = blockIdx.x;
+    const uint64_t lo = total_chunks * w / G, hi = total_chunks * (w + 1) / G;
+    if (lo >= hi) return;
+    uint64_t l = 0, r = n_blobs - 1;                           // last b with chunk_start[b] <= lo
+    while (l < r) {
+        const uint64_t mid = (l + r + 1) / 2;
+        if (chunk_start[mid] <= lo) l = mid; else r = mid - 1;
+    }
+    uint64_t b = l, next = chunk_start[b + 1];
+    SnapshotCopy c = blobs[b];
+    for (uint64_t ch = lo; ch < hi; ++ch) {
+        if (ch >= next) {                                      // every planned blob has >= 1 chunk
+            ++b;
+            next = chunk_start[b + 1];
+            c = blobs[b];
+        }
+        copy_chunk(src, dst, c, ch - chunk_start[b]);
+    }
+}
+
 }  // namespace
 
 uint64_t snapshot_chunk_bytes() { return kChunk; }
 
 hipError_t launch_snapshot_transpose(const uint8_t* src, uint8_t* dst, const SnapshotCopy* blobs,
-                                     const uint32_t* block_blob, const uint32_t* block_chunk, uint64_t n_blocks,
+                                     const uint64_t* chunk_start, uint64_t n_blobs, uint64_t total_chunks,
                                      hipStream_t s) {
-    // grid.x is limited to 2^31-1 workgroups; one launch per 2^30 chunks (16 PiB) is never split in practice
-    const uint64_t per = (uint64_t)1 << 30;
-    for (uint64_t b = 0; b < n_blocks; b += per) {
-        const uint64_t g = n_blocks - b < per ? n_blocks - b : per;
-        snapshot_transpose_kernel<<<dim3((uint32_t)g), dim3(kThreads), 0, s>>>(src, dst, blobs, block_blob + b,
-                                                                              block_chunk + b);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    if (!n_blobs || !total_chunks) return hipSuccess;
+    // ~8 resident workgroups per CU on 256 CUs, each walking >= 4 chunks when the snapshot is large
+    const uint64_t g = total_chunks < 4 * 2048 ? (total_chunks + 3) / 4 : 2048 * 4;
+    snapshot_transpose_kernel<<<dim3((uint32_t)g), dim3(kThreads), 0, s>>>(src, dst, blobs, chunk_start, n_blobs,
+                                                                          total_chunks);
+    return hipGetLastError();
 }
 
 }  // namespace sda
