@@ -12,4 +12,9 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$c -o run -- \
       python3 bench.py --only combine --steps 3 --warmup 1 > $OUT/pmc_$c.log 2>&1 || exit $?
 done
-find $OUT -name "*.csv" | head -20
+
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_snap_$c -o run -- \
+      python3 bench.py --only snapshot --steps 4 > $OUT/pmc_snap_$c.log 2>&1 || exit $?
+done
+find $OUT -name "*.csv" | head -30
