@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 from typing import Optional, Sequence
 
 import numpy as np
@@ -161,6 +162,11 @@ class Engine:
     """One engine handle = one HIP device + one stream (sda_engine_create)."""
 
     def __init__(self, device: int = 0):
+        # torch (when the caller uses it) ships its own HIP runtime; it has to open the device before
+        # the engine's ROCm runtime does, or torch later reports "No HIP GPUs are available"
+        t = sys.modules.get("torch")
+        if t is not None and t.cuda.is_available():
+            t.cuda.init()
         self.lib = load_library()
         h = _vp()
         _check(self.lib.sda_engine_create(device, C.byref(h)))
