@@ -8,12 +8,13 @@
 // ([participation][clerk] ragged byte blobs); the clerking jobs want [clerk][participation].
 // This is a ragged byte gather: HBM-bound, 2 bytes of traffic per payload byte.
 //
-// Blobs are cut into 32 KiB chunks; a workgroup moves a contiguous run of them.  Every lane owns
+// Blobs are cut into 32 KiB chunks; a workgroup moves a contiguous run of 4 of them.  Every lane owns
 // 16-byte aligned DESTINATION quads so stores are dwordx4.  The source shift (src - dst) mod 16 is
 // uniform per blob: shift 0 takes aligned dwordx4 loads; any other shift takes one unaligned dwordx4
 // load per quad (gfx950 runs with unaligned access mode, so the hardware splits the line crossing).
 // A/B (profiles/r01h/ab_snapshot.txt): unaligned 7.25 ms vs 7.57 ms for two aligned loads + a
-// uniform switch over v_alignbyte (SDA_SNAP_UNALIGNED=0), 91% of a same-size device-to-device copy.
+// uniform switch over v_alignbyte (SDA_SNAP_UNALIGNED=0); with 4-chunk workgroups 6.5-6.8 ms for
+// 16 GB, the same rate as a same-size device-to-device copy.
 // All loads of a chunk are issued before its stores.  The <16-byte head and tail of a chunk, whose
 // quad is shared with the neighbouring blob, are written with byte stores.
 #include "kernels.h"
@@ -25,6 +26,12 @@ namespace {
 constexpr uint32_t kThreads = 256;
 #ifndef SDA_SNAP_UNALIGNED
 #define SDA_SNAP_UNALIGNED 1
+#endif
+#ifndef SDA_SNAP_NT_LOAD
+#define SDA_SNAP_NT_LOAD 0
+#endif
+#ifndef SDA_SNAP_CHUNKS_PER_WG
+#define SDA_SNAP_CHUNKS_PER_WG 4
 #endif
 #ifndef SDA_SNAP_QUADS
 #define SDA_SNAP_QUADS 8
@@ -64,6 +71,9 @@ __device__ __forceinline__ void copy_body(const uint8_t* __restrict__ src, uint8
             const u32x4* p = reinterpret_cast<const u32x4*>(src + (s & ~(uint64_t)15));
             if constexpr (O == 0) {
                 v[it] = p[0];
+            } else if constexpr (SDA_SNAP_UNALIGNED && SDA_SNAP_NT_LOAD) {
+                typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+                v[it] = __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(src + s));
             } else if constexpr (SDA_SNAP_UNALIGNED) {
                 __builtin_memcpy(&v[it], src + s, 16);     // one unaligned dwordx4 (unaligned access mode)
             } else {
@@ -101,7 +111,7 @@ __device__ __forceinline__ void copy_chunk(const uint8_t* __restrict__ src, uint
 
 // Workgroup w walks the contiguous chunk range [total*w/G, total*(w+1)/G) of the clerk-major blob
 // list: one binary search over the chunk prefix for its first blob, then a forward walk, so the
-// host plan is one entry per blob and a workgroup never waits on per-chunk table lookups.
+// host plan is one entry per blob rather than one per chunk.
 __global__ __launch_bounds__(kThreads) void snapshot_transpose_kernel(const uint8_t* __restrict__ src,
                                                                       uint8_t* __restrict__ dst,
                                                                       const SnapshotCopy* __restrict__ blobs,
@@ -135,8 +145,11 @@ hipError_t launch_snapshot_transpose(const uint8_t* src, uint8_t* dst, const Sna
                                      const uint64_t* chunk_start, uint64_t n_blobs, uint64_t total_chunks,
                                      hipStream_t s) {
     if (!n_blobs || !total_chunks) return hipSuccess;
-    // ~8 resident workgroups per CU on 256 CUs, each walking >= 4 chunks when the snapshot is large
-    const uint64_t g = total_chunks < 4 * 2048 ? (total_chunks + 3) / 4 : 2048 * 4;
+    // short-lived workgroups of SDA_SNAP_CHUNKS_PER_WG chunks each: the dispatcher balances the
+    // ragged tail better than long walks (A/B in profiles/r01h/ab_snapshot.txt)
+    const uint64_t cpw = total_chunks / SDA_SNAP_CHUNKS_PER_WG < 0x7fffffffull
+                             ? SDA_SNAP_CHUNKS_PER_WG : total_chunks / 0x7fffffffull + 1;
+    const uint64_t g = (total_chunks + cpw - 1) / cpw;
     snapshot_transpose_kernel<<<dim3((uint32_t)g), dim3(kThreads), 0, s>>>(src, dst, blobs, chunk_start, n_blobs,
                                                                           total_chunks);
     return hipGetLastError();
