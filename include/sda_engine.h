@@ -248,7 +248,8 @@ sda_status sda_varint_encode_dev(sda_engine* h, const int64_t* vals, uint64_t ro
  *     its blob p = [clerk_off[c*(P+1) + p], clerk_off[c*(P+1) + p + 1]) relative to that start, followed
  *     by >= 16 readable bytes -- exactly the (bytes, blob_off) pair sda_clerk_decode_combine_dev takes.
  *   clerk_base [n], clerk_off [n][P+1] (HOST, written); *dst_len = bytes of dst used.
- *   dst == NULL: sizing query (offsets and *dst_len only, nothing launched). */
+ *   dst == NULL: sizing query (offsets and *dst_len only, nothing launched).
+ *   Runs on `stream` and returns once the copy has completed (the copy plan is uploaded per call). */
 sda_status sda_snapshot_transpose_dev(sda_engine* h, const uint8_t* src, const uint64_t* part_off,
                                       uint64_t n_participations, uint64_t n_clerks, uint8_t* dst,
                                       uint64_t dst_cap, uint64_t* dst_len, uint64_t* clerk_base,
