@@ -11,7 +11,7 @@ OBJDIR  ?= build/obj
 LIB     ?= sda_amd/libsda_engine.so
 
 GEN_PARTS    := 3 9 27 81
-REVEAL_PARTS := 8 16 32 64
+REVEAL_PARTS := 8 16 32 64 96
 PLAIN   := combine elementwise chacha codec snapshot
 OBJS    := $(patsubst %,$(OBJDIR)/%.o,$(PLAIN)) $(OBJDIR)/engine.o \
            $(OBJDIR)/packed_gen.o $(patsubst %,$(OBJDIR)/packed_gen_%.o,$(GEN_PARTS)) \

@@ -81,22 +81,89 @@ class Timer:
         return statistics.fmean(s.elapsed_time(e) for s, e in self.pairs)
 
 
+def host_model():
+    """The host the CPU baseline ran on: CPU model, the CPUs this process may use, and the thread
+    budget (the GPU box exports OMP_NUM_THREADS = its CPU share per GPU)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity, "thread_budget": min(share, affinity)}
+
+
 def cpu_baseline(dim: int, budget_s: float):
-    """oracle/ C restatement of combiner.rs:16-28 (real `%` per element), 1 core, bounded sample."""
+    """oracle/ C restatement of combiner.rs:16-28 (real `%` per element, -O2) on a bounded sample of
+    the same synthetic matrix: (i) 1 core -- the reference is single-threaded; (ii) all the host
+    cores this job may use, columns split over POSIX threads."""
     from oracle import oracle as O
     from sda_amd import synth
-    rows = 100
-    x = synth.fill(rows, dim, SEED_BASE + 1, 0, MODULUS)
-    times = []
-    t_start = time.perf_counter()
-    while len(times) < 9 and (time.perf_counter() - t_start) < budget_s or len(times) < 2:
-        t0 = time.perf_counter()
-        O.combine(MODULUS, x)
-        times.append(time.perf_counter() - t0)
-    t = statistics.median(times)
-    return {"value": round(8.0 * rows * dim / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{rows} x {dim:,} i64 rows of the same synthetic matrix (uniform [0, m)), "
-                      f"oracle/sda_oracle.c or_combine at -O2, median of {len(times)} runs"}
+    host = host_model()
+    threads = host["thread_budget"]
+
+    def timed(rows, fn):
+        x = synth.fill(rows, dim, SEED_BASE + 1, 0, MODULUS)
+        times = []
+        t_start = time.perf_counter()
+        while (len(times) < 5 and (time.perf_counter() - t_start) < budget_s) or len(times) < 2:
+            t0 = time.perf_counter()
+            fn(x)
+            times.append(time.perf_counter() - t0)
+        return 8.0 * rows * dim / statistics.median(times) / 1e9, len(times)
+
+    one, n1 = timed(100, lambda x: O.combine(MODULUS, x))
+    allc, n2 = timed(400, lambda x: O.combine_mt(MODULUS, x, threads))
+    return {"value": round(allc, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"400 x {dim:,} i64 rows of the headline matrix (uniform [0, m)), oracle/sda_oracle.c "
+                      f"or_combine_mt at -O2 over {threads} threads (column split), median of {n2} runs",
+            "single_core": {"value": round(one, 4), "unit": "GB/s", "cores": 1,
+                            "sample": f"100 x {dim:,} rows, or_combine (the reference loop, 1 thread), "
+                                      f"median of {n1} runs"},
+            "host": host}
+
+
+class TimedEngine:
+    """Wraps the engine for sda_amd.distributed: HIP events around every combine launch, on the
+    stream the launch is issued on (the kernel's own duration for the roofline)."""
+
+    def __init__(self, eng, timer):
+        self.eng, self.timer = eng, timer
+        self.timing = False
+
+    def __getattr__(self, name):
+        return getattr(self.eng, name)
+
+    def _timed(self, fn, *a):
+        if self.timing:
+            self.timer.record(lambda: fn(*a))
+        else:
+            fn(*a)
+
+    def combine_dev(self, *a):
+        self._timed(self.eng.combine_dev, *a)
+
+    def combine_accumulate_dev(self, *a):
+        self._timed(self.eng.combine_accumulate_dev, *a)
+
+
+def exact_sample_check(torch, shares, cols, m, got, reps=1, rows=None):
+    """Bit-exact check of combiner.rs:22-25 on sampled columns: the sequential recurrence
+    r = (r + v) % m (torch.fmod = Rust's truncated %) replayed on device over the rows in order
+    (`reps` passes over the resident tile for the tiled workload, then its first `rows` rows)."""
+    xs = shares[:, cols]
+    r = torch.zeros(cols.numel(), dtype=torch.int64, device=shares.device)
+    for _ in range(reps):
+        for i in range(xs.shape[0]):
+            r = torch.fmod(r + xs[i], m)
+    for i in range(rows or 0):
+        r = torch.fmod(r + xs[i], m)
+    return torch.equal(r, got[cols])
 
 
 def main():
@@ -127,6 +194,7 @@ def main():
     # ---------------- workload: configs[1] (or configs[3]), HBM-resident ----------------
     N, D, m = args.rows, args.dim, MODULUS
     tile = 0
+    value = achieved = kernel_ms = dt = 0.0
     if args.config == 3:
         # configs[3]: 100k participations x 10M-dim, participations split over the ranks; 8 TB do not
         # fit, so each rank streams its share through one resident 1000 x 10M tile (80 GB) with the
@@ -135,6 +203,7 @@ def main():
         N = (total + world - 1) // world
         tile = 1000
     run_combine = args.only in (None, "combine")
+    side = {}
     if run_combine:
         R = tile if tile else N
         shares = torch.empty((R, D), dtype=torch.int64, device=dev)
@@ -142,24 +211,18 @@ def main():
         partial = torch.empty(D, dtype=torch.int64, device=dev)
         out = torch.empty(D, dtype=torch.int64, device=dev)
         ktimer = Timer(torch)
-
-        def launch_tiled():
-            partial.zero_()
-            for t0 in range(0, N, tile):
-                eng.combine_accumulate_dev(m, shares.data_ptr(), min(tile, N - t0), D, D, partial.data_ptr(), stream())
+        teng = TimedEngine(eng, ktimer)
+        # the product's multi-GPU path (sda_amd.distributed): per-rank exact combine of this rank's
+        # participations (row tiles for configs[3]), one int64 all-reduce over RCCL, device finalize
+        tiles = [(shares.data_ptr(), min(tile, N - t0)) for t0 in range(0, N, tile)] if tile else None
 
         def step(timed):
-            launch = (launch_tiled if tile else  # noqa
-                      lambda: eng.combine_dev(m, shares.data_ptr(), N, D, D, partial.data_ptr(), stream()))
-            if timed:
-                ktimer.record(launch)
+            teng.timing = timed
+            if tile:
+                Dd.combine_tiles_sharded(teng, m, tiles, D, D, partial, out)
             else:
-                launch()
-            if world > 1:
-                dist.all_reduce(partial, op=dist.ReduceOp.SUM)
-                eng.combine_finalize_dev(m, partial.data_ptr(), D, out.data_ptr(), stream())
+                Dd.combine_rows_sharded(teng, m, shares.data_ptr(), N, D, D, partial, out)
 
-        assert Dd.reduce_headroom_ok(world, m)
         for _ in range(args.warmup):
             step(False)
         torch.cuda.synchronize()
@@ -175,29 +238,46 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             dt = float(tt.item())
         kernel_ms = ktimer.mean_ms()
-        # spot-check the result of the last step against torch's int64 column sums (non-negative inputs)
-        res = out if world > 1 else partial
-        cols = torch.randint(0, D, (4096,), device=dev)
-        if tile:        # the tile is re-used: full tiles, then the partial last tile
-            ref = (N // tile) * shares[:, cols].sum(dim=0) + shares[: N % tile, cols].sum(dim=0)
-            ref = torch.remainder(ref, m)
-        else:
-            ref = torch.remainder(shares[:, cols].sum(dim=0), m)
-        if world > 1:
+        # check the last step's result on 4096 sampled columns
+        cols = torch.randint(0, D, (4096,), device=dev, generator=torch.Generator(device=dev).manual_seed(7))
+        if world == 1:       # bit-exact: the sequential recurrence replayed on device
+            ok = exact_sample_check(torch, shares, cols, m, out, reps=(N // tile) if tile else 1,
+                                    rows=(N % tile) if tile else 0)
+        else:                # non-negative inputs: (sum over ranks of column sums) mod m
+            ref = (N // tile) * shares[:, cols].sum(dim=0) + shares[: N % tile, cols].sum(dim=0) if tile \
+                else shares[:, cols].sum(dim=0)
             dist.all_reduce(ref, op=dist.ReduceOp.SUM)
-            ref = torch.remainder(ref, m)
-        if not torch.equal(res[cols], ref):
+            ok = torch.equal(torch.remainder(ref, m), out[cols])
+        if not ok:
             raise SystemExit("combine result check FAILED")
-        bytes_per_launch = 8.0 * N * D + 8.0 * D
-        total_bytes = bytes_per_launch * args.steps * world
+        rows_per_launch = tile if tile else N
+        bytes_per_launch = 8.0 * rows_per_launch * D + 8.0 * D
+        total_bytes = (8.0 * N * D + 8.0 * D * (len(tiles) if tile else 1)) * args.steps * world
         value = total_bytes / dt / 1e9
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
         log(f"[combine] rank {rank}: {args.steps} steps in {dt*1e3:.1f} ms, kernel {kernel_ms:.3f} ms "
             f"({achieved:.0f} GB/s per launch)")
+
+        # the signed worst case -- uniform (-m, m) shares, whose exact result is
+        # order dependent -- through the same kernel on the same resident buffer
+        if not args.no_side and world == 1 and not tile:
+            eng.synth_fill_dev(shares.data_ptr(), N, D, SEED_BASE + 12, -(m - 1), m, stream())
+            st = Timer(torch)
+            sg = lambda: eng.combine_dev(m, shares.data_ptr(), N, D, D, partial.data_ptr(), stream())  # noqa
+            for i in range(1 + max(3, args.steps // 4)):
+                st.record(sg) if i else sg()
+            s_ms = st.mean_ms()
+            if not args.no_check and not exact_sample_check(torch, shares, cols, m, partial):
+                raise SystemExit("signed combine result check FAILED")
+            side["combine_signed"] = {
+                "config": "configs[1] with uniform (-m, m) shares (SURVEY 8(d) C2(ii)), exact signed result",
+                "kernel_ms": s_ms, "GBps": bytes_per_launch / (s_ms * 1e-3) / 1e9,
+                "roofline_frac": bytes_per_launch / (s_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                "check": "bit-exact on 4096 sampled columns (sequential recurrence replayed on device)"}
+            log(f"[combine_signed] {json.dumps(side['combine_signed'])}")
         del shares
 
     # ---------------- side legs (rank-local, reported by rank 0) ----------------
-    side = {}
     if not args.no_side and args.only in (None, "shamir"):
         sch = S.CONFIG_PACKED
         p, k, t, n = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count
@@ -436,8 +516,10 @@ def main():
                        "parallelism": f"participation split x{world}" + (", RCCL int64 all-reduce" if world > 1 else ""),
                        "exact": "combiner.rs:16-28 recurrence, bit-exact"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profile(N, D)},
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic_from_profile(tile if tile else N, D)},
             "kernel_ms": round(kernel_ms, 4),
+            "kernel_bytes_per_launch": 8.0 * (tile if tile else N) * D + 8.0 * D,
         }
         rec.update(side)
         if world == 1 and not args.no_cpu:

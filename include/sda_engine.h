@@ -21,7 +21,11 @@
  *   - Every function returns an sda_status; 0 = OK.  The codes 1..6 map 1:1 to
  *     the reference's error strings; sda_last_error_message() gives details.
  *   - A handle may be used from one thread at a time (the Rust trait objects
- *     are not Sync either); distinct handles are independent.
+ *     are not Sync either); distinct handles are independent.  The handle's
+ *     scratch buffers are shared by its calls: a `_dev` call on a different
+ *     stream than the handle's previous call first makes its stream wait (an
+ *     event, no host sync) for the work queued on the previous one, so calls
+ *     on one handle never race however the caller mixes streams.
  */
 #ifndef SDA_ENGINE_H
 #define SDA_ENGINE_H
@@ -185,7 +189,7 @@ sda_status sda_packed_generate_mode_dev(sda_engine* h, const sda_sharing_scheme*
                                         const int64_t* draws, int64_t* out, int32_t mode, void* stream);
 
 /* Packed-Shamir reveal: shares [n_vectors][n_idx][B] at clerk `indices` (host array),
- * out [n_vectors][dimension]. */
+ * out [n_vectors][dimension].  All n_idx shares are used (batched.rs:75); n_idx <= 95. */
 sda_status sda_packed_reconstruct_dev(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,
                                       const uint64_t* indices, uint64_t n_idx, uint64_t n_vectors,
                                       const int64_t* shares, int64_t* out, int32_t mode, void* stream);
@@ -196,8 +200,10 @@ sda_status sda_additive_generate_dev(sda_engine* h, int64_t modulus, uint64_t sh
                                      const int64_t* draws, int64_t* out, void* stream);
 
 /* ChaCha mask expansion + combine (chacha.rs:57-76) over n_seeds seeds of w words
- * (seeds [n_seeds][w] u32, device), out [dimension] canonical.  Exact including
- * gen_range rejections (handled by an on-device fix-up pass). */
+ * (seeds [n_seeds][w] u32, device), out [dimension].  Exact including gen_range rejections
+ * (fix-up pass; moduli with a high rejection rate expand each stream exactly instead) and the
+ * reference's wrapping i64 sum for moduli above 2^62 (the result is then signed and
+ * order-dependent, as in the reference).  Waits for its rejection log before returning. */
 sda_status sda_chacha_mask_combine_dev(sda_engine* h, int64_t modulus, uint64_t dimension,
                                        const uint32_t* seeds, uint64_t w, uint64_t n_seeds,
                                        int64_t* out, void* stream);

@@ -39,6 +39,8 @@ def lib():
         L.or_rem.restype = C.c_int64
         L.or_rem.argtypes = [C.c_int64, C.c_int64]
         L.or_combine.argtypes = [C.c_int64, _i64p, C.c_size_t, C.c_size_t, _i64p]
+        L.or_combine_mt.argtypes = [C.c_int64, _i64p, C.c_size_t, C.c_size_t, _i64p, C.c_int]
+        L.or_combine_mt.restype = C.c_int
         L.or_combine_rows.argtypes = [C.c_int64, C.POINTER(_i64p), _szp, C.c_size_t, _i64p, _szp]
         L.or_combine_rows.restype = C.c_int
         L.or_additive_generate.argtypes = [C.c_int64, C.c_size_t, _i64p, C.c_size_t, _i64p, _i64p]
@@ -93,6 +95,15 @@ def combine(m: int, shares) -> np.ndarray:
     n, dim = (s.shape if s.ndim == 2 else (0, 0))
     out, op = _i64(np.zeros(dim, np.int64))
     lib().or_combine(m, sp, n, dim, op)
+    return out
+
+
+def combine_mt(m: int, shares, threads: int) -> np.ndarray:
+    """combine() with the columns split over `threads` POSIX threads (CPU baseline, all cores)."""
+    s, sp = _i64(shares)
+    n, dim = (s.shape if s.ndim == 2 else (0, 0))
+    out, op = _i64(np.zeros(dim, np.int64))
+    lib().or_combine_mt(m, sp, n, dim, op, threads)
     return out
 
 

@@ -8,6 +8,7 @@
 #include "sda_oracle.h"
 
 #include <stdlib.h>
+#include <pthread.h>
 #include <string.h>
 
 /* ------------------------------------------------------------------------ */
@@ -51,6 +52,45 @@ void or_combine(int64_t m, const int64_t* shares, size_t n, size_t dim, int64_t*
         const int64_t* row = shares + i * dim;
         for (size_t j = 0; j < dim; ++j) out[j] = or_rem(or_wadd(out[j], row[j]), m);
     }
+}
+
+/* The same loop split over `threads` POSIX threads by column range (the CPU baseline's all-cores
+ * mode): columns are independent, so every thread runs combiner.rs:22-25
+ * over all rows, in order, for its own columns -- the result is identical to or_combine. */
+typedef struct {
+    int64_t m;
+    const int64_t* shares;
+    size_t n, dim, c0, c1;
+    int64_t* out;
+} or_combine_part;
+
+static void* or_combine_worker(void* arg) {
+    const or_combine_part* a = (const or_combine_part*)arg;
+    for (size_t j = a->c0; j < a->c1; ++j) a->out[j] = 0;
+    for (size_t i = 0; i < a->n; ++i) {
+        const int64_t* row = a->shares + i * a->dim;
+        for (size_t j = a->c0; j < a->c1; ++j) a->out[j] = or_rem(or_wadd(a->out[j], row[j]), a->m);
+    }
+    return NULL;
+}
+
+int or_combine_mt(int64_t m, const int64_t* shares, size_t n, size_t dim, int64_t* out, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    or_combine_part part[256];
+    int started = 0;
+    for (int t = 0; t < threads; ++t) {
+        /* 64-column aligned ranges: no two threads write one cache line of `out` */
+        const size_t blocks = (dim + 63) / 64;
+        const size_t b0 = blocks * (size_t)t / (size_t)threads, b1 = blocks * (size_t)(t + 1) / (size_t)threads;
+        part[t] = (or_combine_part){m, shares, n, dim, b0 * 64 < dim ? b0 * 64 : dim, b1 * 64 < dim ? b1 * 64 : dim, out};
+        if (pthread_create(&tid[t], NULL, or_combine_worker, &part[t]) != 0) break;
+        ++started;
+    }
+    for (int t = 0; t < started; ++t) pthread_join(tid[t], NULL);
+    for (int t = started; t < threads; ++t) or_combine_worker(&part[t]);   /* could not start: run inline */
+    return started;
 }
 
 /* ------------------------------------------------------------------------ */

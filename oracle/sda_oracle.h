@@ -43,6 +43,7 @@ int or_combine_rows(int64_t m, const int64_t* const* rows, const size_t* lens,
                     size_t n_rows, int64_t* out, size_t* out_len);
 /* dense [n][dim] row-major form of the same loop */
 void or_combine(int64_t m, const int64_t* shares, size_t n, size_t dim, int64_t* out);
+int or_combine_mt(int64_t m, const int64_t* shares, size_t n, size_t dim, int64_t* out, int threads);
 
 /* ---- additive: client/src/crypto/sharing/additive.rs:32-51 via batched.rs:19-53 ----
  * draws: [D][n-1] values that OsRng.gen_range(0, m) returned, in draw order.

@@ -176,20 +176,210 @@ uint64_t h_pair(const uint32_t* key, uint64_t pair) {
     return ((uint64_t)o[2 * (pair % 8)] << 32) | o[2 * (pair % 8) + 1];
 }
 
+
+// ---- exact stream expansion (any rejection rate): the draws of T streams as rows [T][D] ----
+// Pass 1 counts the accepted pairs among the first n_pairs pairs per workgroup, pass 2 scans the
+// counts of each stream, pass 3 recomputes the blocks and writes the i-th accepted draw (mod m) to
+// element i -- exactly gen_range's rejection loop, with no per-stream limit on rejections.
+__device__ __forceinline__ void stream_key(const uint32_t* seeds, uint32_t w, uint64_t s, uint32_t (&key)[8]) {
+    const uint32_t nw = w < 8 ? w : 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) key[q] = (uint32_t)q < nw ? seeds[s * w + q] : 0u;
+}
+
+__device__ __forceinline__ uint32_t block_sum256(uint32_t v, uint32_t* lds) {
+    lds[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) lds[threadIdx.x] += lds[threadIdx.x + h];
+        __syncthreads();
+    }
+    const uint32_t r = lds[0];
+    __syncthreads();
+    return r;
+}
+
+// exclusive prefix of v over the 256 lanes of the workgroup (Hillis-Steele in LDS)
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* lds) {
+    lds[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1) {
+        const uint32_t add = threadIdx.x >= d ? lds[threadIdx.x - d] : 0u;
+        __syncthreads();
+        lds[threadIdx.x] += add;
+        __syncthreads();
+    }
+    const uint32_t incl = lds[threadIdx.x];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(256) void chacha_stream_count_kernel(const uint32_t* __restrict__ seeds, uint32_t w,
+                                                                  uint64_t seed0, uint64_t n_pairs, uint64_t zone,
+                                                                  uint64_t* __restrict__ cnt, uint32_t nwg) {
+    __shared__ uint32_t lds[256];
+    const uint64_t blk = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t key[8];
+    stream_key(seeds, w, seed0 + blockIdx.y, key);
+    uint32_t c = 0;
+    if (blk * 8 < n_pairs) {
+        uint32_t o[16];
+        chacha_block(key, blk, o);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t v = ((uint64_t)o[2 * q] << 32) | o[2 * q + 1];
+            c += (blk * 8 + q < n_pairs && v < zone) ? 1u : 0u;
+        }
+    }
+    c = block_sum256(c, lds);
+    if (threadIdx.x == 0) cnt[(uint64_t)blockIdx.y * nwg + blockIdx.x] = c;
+}
+
+// one workgroup per stream: exclusive scan of its nwg counts in place; tot[t] = accepted pairs
+__global__ __launch_bounds__(256) void chacha_stream_scan_kernel(uint64_t* __restrict__ cnt, uint32_t nwg,
+                                                                 uint64_t* __restrict__ tot) {
+    __shared__ uint32_t lds[256];
+    uint64_t* row = cnt + (uint64_t)blockIdx.x * nwg;
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < nwg; base += 256) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < nwg ? (uint32_t)row[i] : 0u;   // <= 2048 per workgroup
+        const uint32_t ex = block_excl_scan256(v, lds);
+        const uint32_t sum = block_sum256(v, lds);
+        if (i < nwg) row[i] = carry + ex;
+        carry += sum;
+    }
+    if (threadIdx.x == 0) tot[blockIdx.x] = carry;
+}
+
+__global__ __launch_bounds__(256) void chacha_stream_scatter_kernel(const uint32_t* __restrict__ seeds, uint32_t w,
+                                                                    uint64_t seed0, uint64_t n_pairs, uint64_t zone,
+                                                                    Mod64 M, const uint64_t* __restrict__ off,
+                                                                    uint32_t nwg, uint64_t D,
+                                                                    int64_t* __restrict__ rows) {
+    __shared__ uint32_t lds[256];
+    const uint64_t blk = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t base = off[(uint64_t)blockIdx.y * nwg + blockIdx.x];
+    if (base >= D) return;                                   // uniform: the whole workgroup is past D
+    uint32_t key[8];
+    stream_key(seeds, w, seed0 + blockIdx.y, key);
+    uint32_t o[16];
+    uint32_t flags = 0;
+    if (blk * 8 < n_pairs) {
+        chacha_block(key, blk, o);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t v = ((uint64_t)o[2 * q] << 32) | o[2 * q + 1];
+            flags |= (blk * 8 + q < n_pairs && v < zone) ? (1u << q) : 0u;
+        }
+    }
+    uint64_t pos = base + block_excl_scan256((uint32_t)__builtin_popcount(flags), lds);
+    int64_t* row = rows + (uint64_t)blockIdx.y * D;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        if (flags & (1u << q)) {
+            const uint64_t v = ((uint64_t)o[2 * q] << 32) | o[2 * q + 1];
+            if (pos < D) row[pos] = (int64_t)umod64(v, M);
+            ++pos;
+        }
+    }
+}
+
 }  // namespace
 
-// work layout: [acc: D u64][count u64][seed_of: cap u32][pair_of: cap u64][rej upload: cap u64]
+// ---- fast path: work layout [acc: D u64][count u64][seed_of: cap u32][pair_of: cap u64][rej upload: cap u64]
 static constexpr uint64_t kRejectCap = 1 << 16;
 
 size_t chacha_work_bytes(uint64_t dimension) {
     return dimension * 8 + 16 + kRejectCap * (4 + 8 + 8) + 64;
 }
 
-static hipError_t chacha_combine_impl(int64_t modulus, uint64_t D, const uint32_t* seeds_dev,
-                                      const std::vector<uint32_t>& seeds_host, uint32_t w, uint64_t n_seeds,
-                                      int64_t* out, void* work, hipStream_t s, int* fixups_out) {
-    if (fixups_out) *fixups_out = 0;
+bool chacha_needs_stream_path(int64_t modulus) {
+    const uint64_t m = (uint64_t)modulus;
+    const uint64_t rejected = UINT64_MAX % m + 1;           // #{v : v >= zone}, zone = u64::MAX - u64::MAX % m
+    return m > (1ull << 62) || rejected > (1ull << 36);    // signed (wrapping) sums, or > 2^-28 rejections
+}
+
+// ---- stream path: [rows: T x D i64][off: T x nwg u64][tot: T u64] ----
+static uint64_t stream_pairs(uint64_t D, int64_t modulus, uint32_t slack_shift) {
+    const double q = (double)(UINT64_MAX % (uint64_t)modulus + 1) / 18446744073709551616.0;
+    const double extra = (double)D * q / (1.0 - q);
+    uint64_t P = D + (uint64_t)(extra * 1.25 + 64.0 * __builtin_sqrt(extra + 1.0)) + 8192;
+    P <<= slack_shift;                                      // retry: more pairs
+    return (P + 7) & ~(uint64_t)7;
+}
+static uint64_t stream_tile(uint64_t D, uint64_t n_seeds) {
+    uint64_t T = (512ull << 20) / (D * 8 + 1);              // ~512 MiB of draws per tile
+    if (T < 1) T = 1;
+    if (T > 1024) T = 1024;
+    if (n_seeds && T > n_seeds) T = n_seeds;
+    return T;
+}
+static uint32_t stream_nwg(uint64_t P) { return (uint32_t)((P / 8 + 255) / 256); }
+
+// rows[t][0..D) = the draws of stream seed0 + t, t < T; `scratch` holds the scan (stream_scan_bytes).
+// Host-synchronous: checks that every stream had D accepted pairs among the pairs it scanned, and
+// rescans with more pairs if not.
+static size_t stream_scan_bytes(uint64_t D, uint64_t T, int64_t modulus) {
+    return T * (uint64_t)stream_nwg(stream_pairs(D, modulus, 2)) * 8 + T * 8 + 64;
+}
+static hipError_t expand_streams(int64_t modulus, uint64_t D, const uint32_t* seeds, uint32_t w, uint64_t seed0,
+                                 uint64_t T, int64_t* rows, char* scratch, hipStream_t s) {
+    const Mod64 M = make_mod64(modulus);
+    const uint64_t zone = UINT64_MAX - UINT64_MAX % (uint64_t)modulus;
+    for (uint32_t slack = 0; slack <= 2; ++slack) {
+        const uint64_t P = stream_pairs(D, modulus, slack);
+        const uint32_t nwg = stream_nwg(P);
+        uint64_t* off = reinterpret_cast<uint64_t*>(scratch);
+        uint64_t* tot = off + T * nwg;
+        const dim3 grid(nwg, (unsigned)T);
+        hipLaunchKernelGGL(chacha_stream_count_kernel, grid, dim3(256), 0, s, seeds, w, seed0, P, zone, off, nwg);
+        hipLaunchKernelGGL(chacha_stream_scan_kernel, dim3((unsigned)T), dim3(256), 0, s, off, nwg, tot);
+        hipLaunchKernelGGL(chacha_stream_scatter_kernel, grid, dim3(256), 0, s, seeds, w, seed0, P, zone, M, off, nwg,
+                           D, rows);
+        hipError_t e;
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        std::vector<uint64_t> got(T);
+        if ((e = hipMemcpyAsync(got.data(), tot, T * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (*std::min_element(got.begin(), got.end()) >= D) return hipSuccess;
+    }
+    return hipErrorUnknown;    // 4x the expected pairs did not hold D accepted draws: practically impossible
+}
+
+size_t chacha_stream_work_bytes(uint64_t D, uint64_t n_seeds, int64_t modulus) {
+    const uint64_t T = stream_tile(D, n_seeds);
+    return T * D * 8 + stream_scan_bytes(D, T, modulus) + 256;
+}
+
+hipError_t launch_chacha_streams_combine(int64_t modulus, uint64_t D, const uint32_t* seeds, uint32_t w,
+                                         uint64_t n_seeds, int64_t* out, void* work, hipStream_t s) {
     if (D == 0) return hipSuccess;
+    if (n_seeds == 0) return hipMemsetAsync(out, 0, D * 8, s);            // chacha.rs:58 vec![0; dimension]
+    const uint64_t T = stream_tile(D, n_seeds);
+    int64_t* rows = static_cast<int64_t*>(work);
+    char* scratch = static_cast<char*>(work) + ((T * D * 8 + 255) & ~(uint64_t)255);
+    for (uint64_t s0 = 0; s0 < n_seeds; s0 += T) {
+        const uint64_t t = n_seeds - s0 < T ? n_seeds - s0 : T;
+        hipError_t e = expand_streams(modulus, D, seeds, w, s0, t, rows, scratch, s);
+        if (e != hipSuccess) return e;
+        // chacha.rs:68-72: r = (r + draw) % m over the seeds in order -- the exact combine recurrence,
+        // wrapping i64 add included (m > 2^62 gives order-dependent signed sums, as in the reference)
+        if ((e = launch_combine_exact(rows, t, D, D, out, modulus, s, s0 > 0)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_chacha_stream(int64_t modulus, uint64_t D, const uint32_t* seed, uint32_t w, int64_t* mask,
+                                void* work, hipStream_t s) {
+    if (D == 0) return hipSuccess;
+    return expand_streams(modulus, D, seed, w, 0, 1, mask, static_cast<char*>(work), s);
+}
+
+// ---- fast path (counter mode + rejection log) ----
+static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_t* seeds_dev, uint32_t w,
+                                      uint64_t n_seeds, int64_t* out, void* work, hipStream_t s, bool* overflow,
+                                      int* fixups_out) {
     const Mod64 M = make_mod64(modulus);
     const uint64_t zone = UINT64_MAX - UINT64_MAX % (uint64_t)modulus;
     char* base = static_cast<char*>(work);
@@ -226,7 +416,10 @@ static hipError_t chacha_combine_impl(int64_t modulus, uint64_t D, const uint32_
         unsigned long long n_rej = 0;
         if ((e = hipMemcpyAsync(&n_rej, count, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        if (n_rej > kRejectCap) return hipErrorOutOfMemory;   // engine falls back (see engine.cpp)
+        if (n_rej > kRejectCap) {          // the caller reruns the job on the stream path
+            *overflow = true;
+            return hipSuccess;
+        }
         if (n_rej) {
             // canonicalise in place so the fix-ups can work modulo m without overflow
             hipLaunchKernelGGL(acc_mod_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, acc, D,
@@ -234,8 +427,11 @@ static hipError_t chacha_combine_impl(int64_t modulus, uint64_t D, const uint32_
             if ((e = hipGetLastError()) != hipSuccess) return e;
             std::vector<uint32_t> so(n_rej);
             std::vector<uint64_t> po(n_rej);
+            std::vector<uint32_t> seeds_host((size_t)n_seeds * w);     // only now: keys of the affected streams
             if ((e = hipMemcpy(so.data(), seed_of, n_rej * 4, hipMemcpyDeviceToHost)) != hipSuccess) return e;
             if ((e = hipMemcpy(po.data(), pair_of, n_rej * 8, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+            if ((e = hipMemcpy(seeds_host.data(), seeds_dev, seeds_host.size() * 4, hipMemcpyDeviceToHost)) != hipSuccess)
+                return e;
             std::vector<std::pair<uint32_t, uint64_t>> ev(n_rej);
             for (size_t i = 0; i < n_rej; ++i) ev[i] = {so[i], po[i]};
             std::sort(ev.begin(), ev.end());
@@ -254,7 +450,10 @@ static hipError_t chacha_combine_impl(int64_t modulus, uint64_t D, const uint32_
                     if (v >= zone) rej.push_back(scanned);
                     ++scanned;
                 }
-                if (rej.size() > kRejectCap) return hipErrorOutOfMemory;
+                if (rej.size() > kRejectCap) {
+                    *overflow = true;
+                    return hipSuccess;
+                }
                 if ((e = hipMemcpy(rej_up, rej.data(), rej.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return e;
                 const uint64_t i0 = rej.front();
                 const uint64_t nfix = D - i0;
@@ -271,29 +470,12 @@ static hipError_t chacha_combine_impl(int64_t modulus, uint64_t D, const uint32_
 }
 
 hipError_t launch_chacha_mask_combine(int64_t modulus, uint64_t dimension, const uint32_t* seeds, uint32_t w,
-                                      uint64_t n_seeds, int64_t* out, void* work, hipStream_t s, int* fixups_out) {
-    // host copy of the seeds, needed only if a rejection occurs (tiny: n_seeds * w words)
-    std::vector<uint32_t> host((size_t)n_seeds * w);
-    if (!host.empty()) {
-        hipError_t e = hipMemcpyAsync(host.data(), seeds, host.size() * 4, hipMemcpyDeviceToHost, s);
-        if (e != hipSuccess) return e;
-    }
-    return chacha_combine_impl(modulus, dimension, seeds, host, w, n_seeds, out, work, s, fixups_out);
-}
-
-hipError_t launch_chacha_mask(int64_t modulus, const uint32_t* seed_host, uint32_t w, const int64_t* secrets,
-                              uint64_t D, int64_t* masked, void* work, hipStream_t s) {
-    // mask_i = single-stream "combine"; masked = (s + mask) % m  (chacha.rs:42-45)
-    std::vector<uint32_t> host(seed_host, seed_host + w);
-    char* base = static_cast<char*>(work);
-    const size_t need = chacha_work_bytes(D);
-    uint32_t* seed_dev = reinterpret_cast<uint32_t*>(base + need);
-    int64_t* mask_dev = reinterpret_cast<int64_t*>(base + need + 64);
-    hipError_t e;
-    if (w && (e = hipMemcpyAsync(seed_dev, seed_host, w * 4, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = chacha_combine_impl(modulus, D, seed_dev, host, w, 1, mask_dev, work, s, nullptr)) != hipSuccess)
-        return e;
-    return launch_addsub_trem(secrets, mask_dev, +1, D, masked, modulus, s);
+                                      uint64_t n_seeds, int64_t* out, void* work, hipStream_t s, bool* overflow,
+                                      int* fixups_out) {
+    *overflow = false;
+    if (fixups_out) *fixups_out = 0;
+    if (dimension == 0) return hipSuccess;
+    return chacha_combine_fast(modulus, dimension, seeds, w, n_seeds, out, work, s, overflow, fixups_out);
 }
 
 }  // namespace sda

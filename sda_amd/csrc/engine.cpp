@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -36,6 +37,10 @@ struct sda_engine {
     sda::DeviceTable rev_tab;     // packed-Shamir Newton/Lagrange tables (per scheme + clerk set)
     void* snap = nullptr;         // snapshot transposition copy plan
     size_t snap_bytes = 0;
+    // The scratch buffers above are shared by every call on the handle.  A call on another stream
+    // than the previous one first waits (on the device) for the work queued on that stream.
+    hipStream_t last_stream = nullptr;
+    hipEvent_t order_ev = nullptr;
 };
 
 namespace {
@@ -78,7 +83,18 @@ sda_status ensure(void** buf, size_t* have, size_t need) {
 
 // `_dev` entry points run on the caller's stream; NULL is the HIP null (default) stream, which is
 // also what torch's default stream reports -- so work stays ordered with the caller's own ops.
-hipStream_t pick(sda_engine*, void* stream) { return static_cast<hipStream_t>(stream); }
+// Switching streams orders the new stream after the previous one (event wait, no host sync), so a
+// call never reuses a scratch buffer that work queued on another stream may still be reading.
+hipStream_t pick(sda_engine* h, void* stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (s != h->last_stream) {
+        if (hipEventRecord(h->order_ev, h->last_stream) != hipSuccess ||
+            hipStreamWaitEvent(s, h->order_ev, 0) != hipSuccess)
+            (void)hipStreamSynchronize(h->last_stream);      // same ordering, from the host
+        h->last_stream = s;
+    }
+    return s;
+}
 
 bool is_pow(uint64_t x, uint64_t b) {
     if (x < 1) return false;
@@ -139,6 +155,7 @@ struct DevArena {   // bump allocator over the engine's staging buffer
 };
 
 sda_status stage(sda_engine* h, size_t bytes, DevArena* a) {
+    (void)pick(h, h->stream);                  // host entry points run on the engine's own stream
     sda_status st = ensure(&h->stage, &h->stage_bytes, bytes + 4096);
     if (st) return st;
     a->base = static_cast<char*>(h->stage);
@@ -147,6 +164,37 @@ sda_status stage(sda_engine* h, size_t bytes, DevArena* a) {
 }
 
 size_t rup(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// chacha.rs:57-76: combine of n seed streams ([n][w] u32 words on the device) into out (device, D
+// values).  The fast counter-mode kernel where its rejection log suffices; otherwise (moduli above
+// 2^62, high rejection rates, or a log overflow) the exact stream path.
+sda_status chacha_combine(sda_engine* h, int64_t m, uint64_t D, const uint32_t* seeds, uint32_t w, uint64_t n,
+                          int64_t* out, hipStream_t st) {
+    if (D == 0) return SDA_OK;
+    // SDA_CHACHA_PATH=stream: test hook forcing the stream path (both paths are exact; the tests
+    // compare them at sizes the oracle cannot finish)
+    const char* force = getenv("SDA_CHACHA_PATH");
+    if (!sda::chacha_needs_stream_path(m) && !(force && strcmp(force, "stream") == 0)) {
+        if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D))) return e;
+        bool overflow = false;
+        int fixups = 0;
+        HIP_TRY(sda::launch_chacha_mask_combine(m, D, seeds, w, n, out, h->work, st, &overflow, &fixups));
+        if (!overflow) return SDA_OK;
+    }
+    if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_stream_work_bytes(D, n, m))) return e;
+    HIP_TRY(sda::launch_chacha_streams_combine(m, D, seeds, w, n, out, h->work, st));
+    return SDA_OK;
+}
+
+// chacha.rs:36-45: masked = (secrets + draw) % m for one seed (host words); mask = scratch of D values
+sda_status chacha_mask(sda_engine* h, int64_t m, const uint32_t* seed_host, uint32_t w, const int64_t* secrets,
+                       uint64_t D, int64_t* mask, uint32_t* seed_dev, int64_t* masked, hipStream_t st) {
+    if (D == 0) return SDA_OK;
+    if (w) HIP_TRY(hipMemcpyAsync(seed_dev, seed_host, w * 4, hipMemcpyHostToDevice, st));
+    if (sda_status e = chacha_combine(h, m, D, seed_dev, w, 1, mask, st)) return e;   // one stream == its draws
+    HIP_TRY(sda::launch_addsub_trem(secrets, mask, +1, D, masked, m, st));
+    return SDA_OK;
+}
 
 sda_status finish(sda_engine* h) {
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -190,10 +238,13 @@ sda_status sda_engine_create(int device_ordinal, sda_engine** out) {
     sda_engine* h = new sda_engine();
     h->device = device_ordinal;
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
+        if (h->stream) (void)hipStreamDestroy(h->stream);
         delete h;
-        return fail(SDA_ERR_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+        return fail(SDA_ERR_DEVICE, "hipStreamCreate/hipEventCreate: %s", hipGetErrorString(e));
     }
+    h->last_stream = h->stream;
     *out = h;
     return ok();
 }
@@ -201,7 +252,7 @@ sda_status sda_engine_create(int device_ordinal, sda_engine** out) {
 void sda_engine_destroy(sda_engine* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    (void)hipDeviceSynchronize();            // _dev work may still be queued on callers' streams
     if (h->work) (void)hipFree(h->work);
     if (h->gen_log) (void)hipFree(h->gen_log);
     if (h->codec_work) (void)hipFree(h->codec_work);
@@ -211,6 +262,7 @@ void sda_engine_destroy(sda_engine* h) {
     if (h->stage) (void)hipFree(h->stage);
     sda::free_table(h->gen_tab);
     sda::free_table(h->rev_tab);
+    if (h->order_ev) (void)hipEventDestroy(h->order_ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -349,23 +401,29 @@ sda_status sda_secret_reconstruct(sda_engine* h, const sda_sharing_scheme* s, ui
     if (out_cap < dimension) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
     if (B == 0) { *out_len = 0; return ok(); }              // no batch => no error checks run
     if (n_rows && (!rows || !lens || !indices)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
-    for (uint64_t i = 0; i < n_rows; ++i)                   // batched.rs:84 indexes [batch_index]
-        if (lens[i] < B) return fail(SDA_ERR_PRECONDITION, "index out of bounds: row %llu has %llu < %llu batches",
-                                     (unsigned long long)i, (unsigned long long)lens[i], (unsigned long long)B);
-    if (n_rows < s->privacy_threshold + k)                  // packed_shamir.rs:75
+    // batched.rs:82-86: batch 0 gathers [clerk][0] (a panic on an empty row), then
+    // packed_shamir.rs:75 may fail; any later batch b panics on a row shorter than b + 1
+    const bool enough = n_rows >= s->privacy_threshold + k;
+    for (uint64_t i = 0; i < n_rows; ++i)
+        if (lens[i] < (enough ? B : 1))
+            return fail(SDA_ERR_PRECONDITION, "index out of bounds: row %llu has %llu < %llu batches",
+                        (unsigned long long)i, (unsigned long long)lens[i], (unsigned long long)B);
+    if (!enough)
         return fail(SDA_ERR_NOT_ENOUGH_SHARES, "Not enough shares to reconstruct (%llu < %llu)",
                     (unsigned long long)n_rows, (unsigned long long)(s->privacy_threshold + k));
-    if (n_rows > 63) return fail(SDA_ERR_UNSUPPORTED, "more than 63 clerk shares per batch");
+    if (n_rows > sda::kRevealMaxShares)
+        return fail(SDA_ERR_UNSUPPORTED, "more than %u clerk shares per batch", sda::kRevealMaxShares);
     DevArena a;
     if (sda_status st = stage(h, rup(n_rows * B * 8) + rup(dimension * 8), &a)) return st;
     int64_t* din = a.take<int64_t>(n_rows * B);
     int64_t* dout = a.take<int64_t>(dimension);
     for (uint64_t i = 0; i < n_rows; ++i)
         HIP_TRY(hipMemcpyAsync(din + i * B, rows[i], B * 8, hipMemcpyHostToDevice, h->stream));
+    if (sda_status st = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return st;
     sda::PackedRevealArgs ra{din, dimension, 1, dout};
     HIP_TRY(sda::launch_packed_reveal(ra, indices, (uint32_t)n_rows, (uint32_t)k, (uint32_t)s->modulus,
                                       (uint32_t)s->omega_secrets, (uint32_t)s->omega_shares, SDA_REVEAL_EXACT,
-                                      h->rev_tab, h->stream));
+                                      h->rev_tab, h->gen_log, h->stream));
     HIP_TRY(hipMemcpyAsync(out, dout, dimension * 8, hipMemcpyDeviceToHost, h->stream));
     *out_len = dimension;
     return finish(h);
@@ -413,13 +471,14 @@ sda_status sda_secret_mask(sda_engine* h, const sda_masking_scheme* s, const int
     *mask_len = seed_words;
     if (D == 0) return ok();
     const uint32_t w = (uint32_t)(seed_words < 8 ? seed_words : 8);           // key holds 8 words
-    if (sda_status st = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D) + 64 + D * 8)) return st;
     DevArena a;
-    if (sda_status st = stage(h, 2 * rup(D * 8), &a)) return st;
+    if (sda_status st = stage(h, 3 * rup(D * 8) + rup(64), &a)) return st;
     int64_t* ds = a.take<int64_t>(D);
+    int64_t* dmask = a.take<int64_t>(D);
     int64_t* dout = a.take<int64_t>(D);
+    uint32_t* dseed = a.take<uint32_t>(16);
     HIP_TRY(hipMemcpyAsync(ds, secrets, D * 8, hipMemcpyHostToDevice, h->stream));
-    HIP_TRY(sda::launch_chacha_mask(s->modulus, seed, w, ds, D, dout, h->work, h->stream));
+    if (sda_status st = chacha_mask(h, s->modulus, seed, w, ds, D, dmask, dseed, dout, h->stream)) return st;
     HIP_TRY(hipMemcpyAsync(masked_out, dout, D * 8, hipMemcpyDeviceToHost, h->stream));
     return finish(h);
 }
@@ -455,16 +514,13 @@ sda_status sda_mask_combine(sda_engine* h, const sda_masking_scheme* s, const in
         for (uint64_t j = 0; j < lens[i] && j < w; ++j) seeds[i * w + j] = (uint32_t)rows[i][j];   // chacha.rs:62-64
     *out_len = D;
     if (D == 0) return ok();
-    if (sda_status st = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D))) return st;
     DevArena a;
     if (sda_status st = stage(h, rup(seeds.size() * 4 + 4) + rup(D * 8), &a)) return st;
     uint32_t* dseeds = a.take<uint32_t>(seeds.size() + 1);
     int64_t* dout = a.take<int64_t>(D);
     if (!seeds.empty())
         HIP_TRY(hipMemcpyAsync(dseeds, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, h->stream));
-    int fixups = 0;
-    HIP_TRY(sda::launch_chacha_mask_combine(s->modulus, D, dseeds, (uint32_t)w, n_rows, dout, h->work, h->stream,
-                                            &fixups));
+    if (sda_status st = chacha_combine(h, s->modulus, D, dseeds, (uint32_t)w, n_rows, dout, h->stream)) return st;
     HIP_TRY(hipMemcpyAsync(out, dout, D * 8, hipMemcpyDeviceToHost, h->stream));
     return finish(h);
 }
@@ -587,15 +643,19 @@ sda_status sda_packed_reconstruct_dev(sda_engine* h, const sda_sharing_scheme* s
     if (!h || !s || s->kind != SDA_SHARING_PACKED_SHAMIR) return fail(SDA_ERR_INVALID_ARGUMENT, "need a PackedShamir scheme");
     if (sda_status st = check_packed(s)) return st;
     if (mode != SDA_REVEAL_EXACT && mode != SDA_REVEAL_CANONICAL) return fail(SDA_ERR_INVALID_ARGUMENT, "bad mode");
+    if (dimension == 0) return ok();                        // batched.rs:77-81: no batch, no check
     if (n_idx < s->privacy_threshold + s->secret_count)
         return fail(SDA_ERR_NOT_ENOUGH_SHARES, "Not enough shares to reconstruct");
-    if (n_idx > 63) return fail(SDA_ERR_UNSUPPORTED, "more than 63 clerk shares per batch");
+    if (n_idx > sda::kRevealMaxShares)
+        return fail(SDA_ERR_UNSUPPORTED, "more than %u clerk shares per batch", sda::kRevealMaxShares);
     if (n_vectors > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 vectors per launch");
     HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = pick(h, stream);
+    if (sda_status e = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return e;
     sda::PackedRevealArgs ra{shares, dimension, n_vectors, out};
     hipError_t e = sda::launch_packed_reveal(ra, indices, (uint32_t)n_idx, (uint32_t)s->secret_count,
                                              (uint32_t)s->modulus, (uint32_t)s->omega_secrets,
-                                             (uint32_t)s->omega_shares, mode, h->rev_tab, pick(h, stream));
+                                             (uint32_t)s->omega_shares, mode, h->rev_tab, h->gen_log, st);
     if (e == hipErrorInvalidValue && mode == SDA_REVEAL_CANONICAL)
         return fail(SDA_ERR_UNSUPPORTED, "canonical reveal needs distinct clerk indices");
     HIP_TRY(e);
@@ -618,10 +678,8 @@ sda_status sda_chacha_mask_combine_dev(sda_engine* h, int64_t modulus, uint64_t 
     if (dimension && modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
     if (w == 0 || w > 8) return fail(SDA_ERR_INVALID_ARGUMENT, "seed width must be 1..8 words");
     HIP_TRY(hipSetDevice(h->device));
-    if (sda_status st = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(dimension))) return st;
-    int fixups = 0;
-    HIP_TRY(sda::launch_chacha_mask_combine(modulus, dimension, seeds, (uint32_t)w, n_seeds, out, h->work,
-                                            pick(h, stream), &fixups));
+    if (sda_status st = chacha_combine(h, modulus, dimension, seeds, (uint32_t)w, n_seeds, out, pick(h, stream)))
+        return st;
     return ok();
 }
 
@@ -878,35 +936,51 @@ sda_status recipient_pipeline(sda_engine* h, const sda_masking_scheme* ms, const
                               int64_t output_modulus, int32_t mode, int64_t* out, uint64_t out_cap,
                               uint64_t* out_len, hipStream_t st) {
     *out_len = 0;
-    // ---- masked output length (reconstruct) ----
-    uint64_t D;
-    if (ss->kind == SDA_SHARING_ADDITIVE) {
-        D = n_idx ? share_len : 0;                           // additive.rs:56-60
-    } else if (ss->kind == SDA_SHARING_PACKED_SHAMIR) {
-        if (sda_status e = check_packed(ss)) return e;
-        if (n_idx < ss->privacy_threshold + ss->secret_count)
-            return fail(SDA_ERR_NOT_ENOUGH_SHARES, "Not enough shares to reconstruct");   // packed_shamir.rs:75
-        if (n_idx > 63) return fail(SDA_ERR_UNSUPPORTED, "more than 63 clerk shares per batch");
-        if (mode != SDA_REVEAL_EXACT && mode != SDA_REVEAL_CANONICAL) return fail(SDA_ERR_INVALID_ARGUMENT, "bad mode");
-        const uint64_t B = (dimension + ss->secret_count - 1) / ss->secret_count;
-        if (dimension && share_len < B)
-            return fail(SDA_ERR_PRECONDITION, "index out of bounds: clerk vector shorter than the batch count");
-        D = dimension;
-    } else {
-        return fail(SDA_ERR_INVALID_ARGUMENT, "unknown sharing scheme kind");
-    }
-    // ---- mask length (mask combine) ----
+    // Checks in the reference's order: mask combine (receive.rs:101-117), reconstruct (:120-146),
+    // unmask (:149-152).
+    // ---- 1. mask combine: its length and panics ----
     uint64_t mask_len = 0;
     if (ms->kind == SDA_MASKING_NONE) {
         if (n_masks && mask_width) return fail(SDA_ERR_PRECONDITION, "assertion failed: masks.iter().all(|mask| mask.len() == 0)");
     } else if (ms->kind == SDA_MASKING_FULL) {
-        mask_len = n_masks ? mask_width : 0;                // full.rs:40
+        mask_len = n_masks ? mask_width : 0;                // full.rs:38-40
+        if (mask_len) {                                     // full.rs:45 `%= modulus`
+            int64_t q0;
+            if (sda_status e = modulus_abs(ms->modulus, &q0)) return e;
+        }
     } else if (ms->kind == SDA_MASKING_CHACHA) {
         mask_len = ms->dimension;                           // chacha.rs:58
         if (mask_width == 0 || mask_width > 8) return fail(SDA_ERR_UNSUPPORTED, "device seeds must be 1..8 words");
+        if (mask_len && n_masks && ms->modulus <= 0)        // chacha.rs:69 gen_range(0, m)
+            return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
     } else {
         return fail(SDA_ERR_INVALID_ARGUMENT, "unknown masking scheme kind");
     }
+    // ---- 2. reconstruct: masked output length and errors ----
+    uint64_t D;
+    if (ss->kind == SDA_SHARING_ADDITIVE) {
+        D = n_idx ? share_len : 0;                           // additive.rs:56-60
+        if (D) {                                             // additive.rs:67 `%= modulus`
+            int64_t m0;
+            if (sda_status e = modulus_abs(ss->modulus, &m0)) return e;
+        }
+    } else if (ss->kind == SDA_SHARING_PACKED_SHAMIR) {
+        if (sda_status e = check_packed(ss)) return e;
+        if (mode != SDA_REVEAL_EXACT && mode != SDA_REVEAL_CANONICAL) return fail(SDA_ERR_INVALID_ARGUMENT, "bad mode");
+        const uint64_t B = (dimension + ss->secret_count - 1) / ss->secret_count;
+        if (B) {                                             // batched.rs:77-81: no batch => no check
+            const bool enough = n_idx >= ss->privacy_threshold + ss->secret_count;
+            if (n_idx && share_len < (enough ? B : 1))      // batched.rs:84 indexes [batch_index]
+                return fail(SDA_ERR_PRECONDITION, "index out of bounds: clerk vector shorter than the batch count");
+            if (!enough) return fail(SDA_ERR_NOT_ENOUGH_SHARES, "Not enough shares to reconstruct");  // packed_shamir.rs:75
+            if (n_idx > sda::kRevealMaxShares)
+                return fail(SDA_ERR_UNSUPPORTED, "more than %u clerk shares per batch", sda::kRevealMaxShares);
+        }
+        D = dimension;
+    } else {
+        return fail(SDA_ERR_INVALID_ARGUMENT, "unknown sharing scheme kind");
+    }
+    // ---- 3. unmask ----
     if (ms->kind != SDA_MASKING_NONE && mask_len != D)     // chacha.rs:83 / full.rs:58 assert_eq!
         return fail(SDA_ERR_PRECONDITION, "assertion failed: mask.len() == masked_secrets.len() (%llu vs %llu)",
                     (unsigned long long)mask_len, (unsigned long long)D);
@@ -927,11 +1001,9 @@ sda_status recipient_pipeline(sda_engine* h, const sda_masking_scheme* ms, const
         if (sda_status e = modulus_abs(ms->modulus, &q)) return e;
         HIP_TRY(sda::launch_combine_exact(static_cast<const int64_t*>(mask_in), n_masks, D, mask_width, dmask, q, st));
     } else if (ms->kind == SDA_MASKING_CHACHA) {
-        if (ms->modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
-        if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D))) return e;
-        int fixups = 0;
-        HIP_TRY(sda::launch_chacha_mask_combine(ms->modulus, D, static_cast<const uint32_t*>(mask_in),
-                                                (uint32_t)mask_width, n_masks, dmask, h->work, st, &fixups));
+        if (sda_status e = chacha_combine(h, ms->modulus, D, static_cast<const uint32_t*>(mask_in),
+                                          (uint32_t)mask_width, n_masks, dmask, st))
+            return e;
     }
     // 2. reconstruct (receive.rs:120-146)
     if (!packed) {
@@ -945,10 +1017,11 @@ sda_status recipient_pipeline(sda_engine* h, const sda_masking_scheme* ms, const
             HIP_TRY(hipMemcpy2DAsync(c, B * 8, shares, share_len * 8, B * 8, n_idx, hipMemcpyDeviceToDevice, st));
             src = c;
         }
+        if (sda_status e = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return e;
         sda::PackedRevealArgs ra{src, dimension, 1, dmasked};
         hipError_t e = sda::launch_packed_reveal(ra, indices, (uint32_t)n_idx, (uint32_t)ss->secret_count,
                                                  (uint32_t)ss->modulus, (uint32_t)ss->omega_secrets,
-                                                 (uint32_t)ss->omega_shares, mode, h->rev_tab, st);
+                                                 (uint32_t)ss->omega_shares, mode, h->rev_tab, h->gen_log, st);
         if (e == hipErrorInvalidValue && mode == SDA_REVEAL_CANONICAL)
             return fail(SDA_ERR_UNSUPPORTED, "canonical reveal needs distinct clerk indices");
         HIP_TRY(e);
@@ -1061,7 +1134,7 @@ sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms
     const int64_t* masked = secrets;
     if (ms->kind != SDA_MASKING_NONE && D) {
         if (ms->modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
-        if (sda_status e = ensure(&h->pipe, &h->pipe_bytes, rup(D * 8) + 256)) return e;
+        if (sda_status e = ensure(&h->pipe, &h->pipe_bytes, 2 * rup(D * 8) + 256)) return e;
         int64_t* dm = static_cast<int64_t*>(h->pipe);
         if (ms->kind == SDA_MASKING_FULL) {
             if (!full_masks) return fail(SDA_ERR_INVALID_ARGUMENT, "Full masking needs the drawn masks");
@@ -1071,9 +1144,11 @@ sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms
             const uint64_t want = (ms->seed_bitsize + 31) / 32;
             if (seed_words != want || (seed_words && !seed))
                 return fail(SDA_ERR_PRECONDITION, "expected %llu seed words", (unsigned long long)want);
-            if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D) + 64 + D * 8)) return e;
-            HIP_TRY(sda::launch_chacha_mask(ms->modulus, seed, (uint32_t)(seed_words < 8 ? seed_words : 8), secrets, D,
-                                            dm, h->work, st));                                       // chacha.rs:36-45
+            int64_t* dmask = dm + rup(D * 8) / 8;
+            uint32_t* dseed = reinterpret_cast<uint32_t*>(dmask + rup(D * 8) / 8);
+            if (sda_status e = chacha_mask(h, ms->modulus, seed, (uint32_t)(seed_words < 8 ? seed_words : 8), secrets,
+                                           D, dmask, dseed, dm, st))                                 // chacha.rs:36-45
+                return e;
         } else {
             return fail(SDA_ERR_INVALID_ARGUMENT, "unknown masking scheme kind");
         }

@@ -67,10 +67,15 @@ hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t
 struct PackedRevealArgs {
     const int64_t* shares; uint64_t dimension; uint64_t n_vectors; int64_t* out;
 };
-// returns hipErrorInvalidValue for CANONICAL mode with duplicate clerk points
+// Reveal takes up to kRevealMaxShares clerk shares per batch (n + 1 <= 81 gives n <= 80 clerks;
+// the kernels keep n_idx + 1 Newton points in registers).
+constexpr int kRevealMaxPoints = 96;
+constexpr uint32_t kRevealMaxShares = kRevealMaxPoints - 1;
+// returns hipErrorInvalidValue for CANONICAL mode with duplicate clerk points.  `log_buf`: device
+// memory of packed_gen_log_bytes() bytes (batches the exact kernel hands to its generic fix-up).
 hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indices, uint32_t n_idx, uint32_t k,
                                 uint32_t p, uint32_t omega_secrets, uint32_t omega_shares, int mode,
-                                DeviceTable& tab, hipStream_t s);
+                                DeviceTable& tab, void* log_buf, hipStream_t s);
 
 // ---- codec.hip (share payload codec: sodium.rs:36-41 / :82-88, integer-encoding 1.0 VarInt) ----
 // Host-side plan of the decode: blobs are split into 4 KiB regions aligned to the (16-byte
@@ -97,16 +102,24 @@ hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len
                                 uint64_t dst_cap, void* work, uint64_t* row_bytes_host, hipStream_t s);
 
 // ---- chacha.hip ----
-// Combine of n_seeds ChaCha mask streams (chacha.rs:57-76).  `work` must hold
-// chacha_work_bytes(...) bytes of device memory.
-size_t chacha_work_bytes(uint64_t n_seeds);
+// Combine of n_seeds ChaCha mask streams (chacha.rs:57-76), two implementations:
+//  * fast path: counter mode, canonical sums, rejections logged and fixed up.  `work` must hold
+//    chacha_work_bytes(D).  Valid when !chacha_needs_stream_path(m); sets *overflow (and writes
+//    nothing) when more rejections occur than its log holds -- rerun on the stream path.
+//  * stream path: the draws of a tile of streams expanded exactly (any rejection rate) into rows,
+//    then the exact sequential combine recurrence (wrapping i64 add for m > 2^62, as the reference).
+//    `work` must hold chacha_stream_work_bytes(D, n_seeds, m).  Host-synchronous per tile.
+size_t chacha_work_bytes(uint64_t dimension);
+bool chacha_needs_stream_path(int64_t modulus);
+size_t chacha_stream_work_bytes(uint64_t dimension, uint64_t n_seeds, int64_t modulus);
 hipError_t launch_chacha_mask_combine(int64_t modulus, uint64_t dimension, const uint32_t* seeds,
                                       uint32_t w, uint64_t n_seeds, int64_t* out, void* work,
-                                      hipStream_t s, int* fixups_out);
-// masked[i] = (secrets[i] + gen_range_i) % m for one seed (chacha.rs:36-45)
-hipError_t launch_chacha_mask(int64_t modulus, const uint32_t* seed_host, uint32_t w,
-                              const int64_t* secrets, uint64_t D, int64_t* masked, void* work,
-                              hipStream_t s);
+                                      hipStream_t s, bool* overflow, int* fixups_out);
+hipError_t launch_chacha_streams_combine(int64_t modulus, uint64_t dimension, const uint32_t* seeds, uint32_t w,
+                                         uint64_t n_seeds, int64_t* out, void* work, hipStream_t s);
+// mask[i] = gen_range draw i of one stream (chacha.rs:36-39); `work`: chacha_stream_work_bytes(D, 1, m)
+hipError_t launch_chacha_stream(int64_t modulus, uint64_t dimension, const uint32_t* seed, uint32_t w,
+                                int64_t* mask, void* work, hipStream_t s);
 
 // ---- snapshot.hip ----
 // One blob of the snapshot transposition: len bytes from src offset to dst offset.

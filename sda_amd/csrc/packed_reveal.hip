@@ -20,7 +20,7 @@ constexpr int KMAX = 64;
 // (Makefile: -DSDA_REVEAL_PART=MM) so the wide instantiations build in parallel.
 template <int MM>
 hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32_t n_idx, uint32_t k,
-                         const uint32_t* tab, const MontP& M, hipStream_t s);
+                         const uint32_t* tab, const MontP& M, unsigned int* log, hipStream_t s);
 
 #ifdef SDA_REVEAL_PART
 namespace {
@@ -30,30 +30,6 @@ struct FE {
     int32_t s;
     uint32_t c;
 };
-
-// generic exact reveal for one batch (inputs outside (-p, p)).  Reads the batch's shares from
-// global memory and writes its `lim` first secrets to dst[0..lim).
-__device__ __noinline__ void reveal_exact_generic(const int64_t* __restrict__ sh, uint64_t B, uint32_t m, uint32_t k,
-                                                  const uint32_t* __restrict__ tab, const MontP& M,
-                                                  int64_t* dst, uint32_t lim) {
-    const Mod64 P = make_mod64((int64_t)M.p);
-    int64_t s[TS];
-    s[0] = 0;
-    for (uint32_t i = 1; i < m; ++i) s[i] = sh[(uint64_t)(i - 1) * B];
-    for (uint32_t j = 1; j < m; ++j)
-        for (uint32_t i = m - 1; i >= j; --i) {
-            const int64_t cd = trem64(wsub(s[i], s[i - 1]), P);
-            s[i] = trem64(wmul(cd, (int64_t)tab[OFF_INV + j * TS + i]), P);
-        }
-    for (uint32_t e = 0; e < k && e < lim; ++e) {
-        int64_t acc = 0;
-        for (uint32_t i = 0; i < m; ++i) {
-            const int64_t np = (int64_t)(int32_t)tab[OFF_NP + e * TS + i];
-            acc = trem64(wadd(acc, trem64(wmul(s[i], np), P)), P);
-        }
-        dst[e] = acc;
-    }
-}
 
 // The k secrets of a batch are adjacent in `out` (batched.rs:94 appends batch after batch), so a
 // lane's own stores would stride by 8k bytes.  With STAGED the workgroup parks its results in
@@ -76,11 +52,18 @@ __device__ __forceinline__ void reveal_flush(int64_t* lds_o, int64_t* o, uint64_
 // whose batch hit it recomputes the batch on the generic exact path.
 // FULL: the point count is exactly MMAX (n_idx + 1 == MMAX), so every `i < m` guard is a compile-time
 // constant: no per-step uniform branches, and the table rows load as merged s_load_dwordx16.
+//
+// A lane whose batch has a share outside (-p, p) (raw i64 input), or whose lazy truncation hit the
+// -p trap, logs the batch and stores garbage; packed_reveal_fixup_kernel, launched right after on the
+// same stream, recomputes those batches on the generic exact path.  Keeping the generic path out of
+// this kernel keeps it free of scratch (its 128-entry i64 array used to cost 1 KiB of scratch per
+// lane, which capped the number of resident waves).
 template <int MMAX, bool STAGED, int KU, bool LAZY, bool FULL = false>
 __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t* __restrict__ shares, uint64_t B,
                                                                   uint64_t D, int64_t* __restrict__ out,
                                                                   uint32_t n_idx, uint32_t k,
-                                                                  const uint32_t* __restrict__ tab, MontP M) {
+                                                                  const uint32_t* __restrict__ tab, MontP M,
+                                                                  unsigned int* __restrict__ log) {
     extern __shared__ int64_t lds_o[];
     const uint32_t tid = threadIdx.x;
     const uint64_t b0 = (uint64_t)blockIdx.x * 256, b = b0 + tid;
@@ -94,22 +77,20 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
     int64_t* dst = STAGED ? lds_o + tid * k : o + b * k;
     const uint32_t lim = STAGED ? k : (b * k < D ? (uint32_t)(D - b * k < k ? D - b * k : k) : 0u);
 
-    // gather [clerk][batch] -> [clerk] (batched.rs:83-85); point 1 carries value 0.  All loads are
-    // issued before the first wait (clamped, branch-free indices).
-    int64_t v[MMAX];
-    static_for<1, MMAX>([&](auto i) { v[i] = sh[(uint64_t)((uint32_t)i < m ? i - 1 : 0) * B]; });
+    // gather [clerk][batch] -> [clerk] (batched.rs:83-85); point 1 carries value 0.  Clamped,
+    // branch-free indices, so every load can be issued before the first wait; each share is turned
+    // into its (sign, residue) pair as it lands, so no i64 copy stays live.
+    FE s[MMAX];
+    s[0] = FE{0, 0};
     bool in_range = true;
     static_for<1, MMAX>([&](auto i) {
-        in_range = in_range && ((uint32_t)i >= m || (uint64_t)(v[i] + (P - 1)) < (uint64_t)(2 * P - 1));
+        const int64_t v = sh[(uint64_t)((uint32_t)i < m ? i - 1 : 0) * B];
+        in_range = in_range && ((uint32_t)i >= m || (uint64_t)(v + (P - 1)) < (uint64_t)(2 * P - 1));
+        const int32_t x = (uint32_t)i < m ? (int32_t)v : 0;
+        s[i] = FE{x, canon32(x, p)};
     });
     Trunc<LAZY> tr;
     if (in_range) {
-        FE s[MMAX];
-        s[0] = FE{0, 0};
-        static_for<1, MMAX>([&](auto i) {
-            const int32_t x = (uint32_t)i < m ? (int32_t)v[i] : 0;
-            s[i] = FE{x, canon32(x, p)};
-        });
         // numtheory::compute_newton_coefficients: for j in 1..m { for i in (j..m).rev() {
         //   s[i] = (((s[i] - s[i-1]) % p) * inv(points[i] - points[i-j])) % p } }
         // inv >= 0, so the product has the sign of the exact difference (or is 0).
@@ -168,8 +149,9 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
             for (uint32_t e = 0; e < k; ++e) eval(e);
         }
     }
-    if (!in_range || tr.bad(p)) {
-        if (live) reveal_exact_generic(sh, B, m, k, tab, M, dst, lim);
+    if ((!in_range || tr.bad(p)) && live) {           // -> packed_reveal_fixup_kernel
+        const uint32_t slot = atomicAdd(log, 1u);
+        if (slot < kGenLogCap) reinterpret_cast<uint64_t*>(log + 16)[slot] = vec * B + b;
     }
     reveal_flush<STAGED>(lds_o, o, b0, B, D, k);
 }
@@ -191,18 +173,17 @@ __global__ __launch_bounds__(256) void packed_reveal_canon_kernel(const int64_t*
     int64_t* dst = STAGED ? lds_o + tid * k : o + b * k;
     const uint32_t lim = STAGED ? k : (b * k < D ? (uint32_t)(D - b * k < k ? D - b * k : k) : 0u);
 
-    int64_t v[NMAX];
-    static_for<0, NMAX>([&](auto i) { v[i] = sh[(uint64_t)((uint32_t)i < n_idx ? i : 0) * B]; });
     uint32_t S[NMAX];
     bool in_range = true;
     static_for<0, NMAX>([&](auto i) {
-        in_range = in_range && ((uint32_t)i >= n_idx || (uint64_t)(v[i] + (P - 1)) < (uint64_t)(2 * P - 1));
-        S[i] = (uint32_t)i < n_idx ? canon32((int32_t)v[i], p) : 0u;
+        const int64_t v = sh[(uint64_t)((uint32_t)i < n_idx ? i : 0) * B];
+        in_range = in_range && ((uint32_t)i >= n_idx || (uint64_t)(v + (P - 1)) < (uint64_t)(2 * P - 1));
+        S[i] = (uint32_t)i < n_idx ? canon32((int32_t)v, p) : 0u;
     });
-    if (!in_range) {                    // raw i64 shares: exact canonical residues (rare)
+    if (!in_range) {                    // raw i64 shares: exact canonical residues (rare; reloaded)
         const Mod64 PM = make_mod64(P);
         static_for<0, NMAX>([&](auto i) {
-            const int64_t r = trem64(v[i], PM);
+            const int64_t r = trem64(sh[(uint64_t)((uint32_t)i < n_idx ? i : 0) * B], PM);
             S[i] = (uint32_t)i < n_idx ? (uint32_t)(r < 0 ? r + P : r) : 0u;
         });
     }
@@ -226,26 +207,32 @@ __global__ __launch_bounds__(256) void packed_reveal_canon_kernel(const int64_t*
 
 template <int MM>
 hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32_t n_idx, uint32_t k,
-                         const uint32_t* tab, const MontP& M, hipStream_t s) {
+                         const uint32_t* tab, const MontP& M, unsigned int* log, hipStream_t s) {
     dim3 grid((unsigned)((B + 255) / 256), (unsigned)a.n_vectors);
     const bool staged = k <= 16;                      // LDS stage: 256 * k * 8 B <= 32 KiB
     const size_t lds = staged ? (size_t)256 * k * sizeof(int64_t) : 0;
     if (mode == 0) {
-        if (staged && k <= 8 && MM <= 16 && M.p >= kLazyTruncMinP && n_idx + 1 == MM)
-            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, true, true>), grid, dim3(256), lds, s,
-                               a.shares, B, a.dimension, a.out, n_idx, k, tab, M);
-        else if (staged && k <= 8 && MM <= 16 && M.p >= kLazyTruncMinP)
-            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, true>), grid, dim3(256), lds, s, a.shares,
-                               B, a.dimension, a.out, n_idx, k, tab, M);
-        else if (staged && k <= 8 && MM <= 16)
-            hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, false>), grid, dim3(256), lds, s, a.shares,
-                               B, a.dimension, a.out, n_idx, k, tab, M);
-        else if (staged)
+        bool done = false;
+        if constexpr (MM <= 16) {
+            done = staged && k <= 8;
+            if (done && M.p >= kLazyTruncMinP && n_idx + 1 == MM)
+                hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, true, true>), grid, dim3(256), lds, s,
+                                   a.shares, B, a.dimension, a.out, n_idx, k, tab, M, log);
+            else if (done && M.p >= kLazyTruncMinP)
+                hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, true>), grid, dim3(256), lds, s,
+                                   a.shares, B, a.dimension, a.out, n_idx, k, tab, M, log);
+            else if (done)
+                hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, false>), grid, dim3(256), lds, s,
+                                   a.shares, B, a.dimension, a.out, n_idx, k, tab, M, log);
+        }
+        if (done) {
+        } else if (staged) {
             hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 0, false>), grid, dim3(256), lds, s, a.shares,
-                               B, a.dimension, a.out, n_idx, k, tab, M);
-        else
+                               B, a.dimension, a.out, n_idx, k, tab, M, log);
+        } else {
             hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, false, 0, false>), grid, dim3(256), 0, s, a.shares,
-                               B, a.dimension, a.out, n_idx, k, tab, M);
+                               B, a.dimension, a.out, n_idx, k, tab, M, log);
+        }
     } else {
         if (staged)
             hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, true>), grid, dim3(256), lds, s, a.shares, B,
@@ -257,9 +244,58 @@ hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32
     return hipGetLastError();
 }
 template hipError_t reveal_launch<SDA_REVEAL_PART>(int, const PackedRevealArgs&, uint64_t, uint32_t, uint32_t,
-                                                   const uint32_t*, const MontP&, hipStream_t);
+                                                   const uint32_t*, const MontP&, unsigned int*, hipStream_t);
 
-#else  // dispatcher + host tables
+#else  // dispatcher, host tables, generic fix-up
+
+namespace {
+
+// Generic exact reveal of one batch (shares outside (-p, p), or a lazy-truncation trap): tss'
+// Newton divided differences and evaluation with wrapping i64 arithmetic and truncated `%`, reading
+// the batch's shares from global memory.  Writes its first `lim` secrets to dst[0..lim).
+__device__ void reveal_exact_generic(const int64_t* __restrict__ sh, uint64_t B, uint32_t m, uint32_t k,
+                                     const uint32_t* __restrict__ tab, uint32_t p, int64_t* dst, uint32_t lim) {
+    const Mod64 P = make_mod64((int64_t)p);
+    int64_t s[TS];
+    s[0] = 0;
+    for (uint32_t i = 1; i < m; ++i) s[i] = sh[(uint64_t)(i - 1) * B];
+    for (uint32_t j = 1; j < m; ++j)
+        for (uint32_t i = m - 1; i >= j; --i) {
+            const int64_t cd = trem64(wsub(s[i], s[i - 1]), P);
+            s[i] = trem64(wmul(cd, (int64_t)tab[OFF_INV + j * TS + i]), P);
+        }
+    for (uint32_t e = 0; e < k && e < lim; ++e) {
+        int64_t acc = 0;
+        for (uint32_t i = 0; i < m; ++i) {
+            const int64_t np = (int64_t)(int32_t)tab[OFF_NP + e * TS + i];
+            acc = trem64(wadd(acc, trem64(wmul(s[i], np), P)), P);
+        }
+        dst[e] = acc;
+    }
+}
+
+// Batches the exact kernel logged, recomputed with the generic path.  If the log overflowed, every
+// batch of the launch is recomputed (correct and slow; only reachable with raw i64 shares).
+__global__ __launch_bounds__(256) void packed_reveal_fixup_kernel(const int64_t* __restrict__ shares, uint64_t B,
+                                                                  uint64_t D, uint64_t n_vec, int64_t* __restrict__ out,
+                                                                  uint32_t n_idx, uint32_t k,
+                                                                  const uint32_t* __restrict__ tab, uint32_t p,
+                                                                  const unsigned int* __restrict__ log) {
+    const uint32_t n = *log;
+    if (n == 0) return;
+    const bool all = n > kGenLogCap;
+    const uint64_t total = all ? B * n_vec : (uint64_t)n;
+    const uint64_t* list = reinterpret_cast<const uint64_t*>(log + 16);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t gb = all ? i : list[i];
+        const uint64_t vec = gb / B, b = gb - vec * B;
+        const uint32_t lim = b * k < D ? (uint32_t)(D - b * k < k ? D - b * k : k) : 0u;
+        reveal_exact_generic(shares + vec * (uint64_t)n_idx * B + b, B, n_idx + 1, k, tab, p, out + vec * D + b * k,
+                             lim);
+    }
+}
+
+}  // namespace
 
 // Host precompute of the per-index-set tables (data independent; same ops as tss).
 static void build_reveal_tables(std::vector<uint32_t>& tab, const uint64_t* indices, uint32_t n_idx, uint32_t k,
@@ -307,7 +343,7 @@ static void build_reveal_tables(std::vector<uint32_t>& tab, const uint64_t* indi
 
 hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indices, uint32_t n_idx, uint32_t k,
                                 uint32_t p, uint32_t omega_secrets, uint32_t omega_shares, int mode,
-                                DeviceTable& tab, hipStream_t s) {
+                                DeviceTable& tab, void* log_buf, hipStream_t s) {
     const uint64_t B = (a.dimension + k - 1) / k;
     if (B == 0 || a.n_vectors == 0) return hipSuccess;
     std::vector<uint8_t> key(sizeof(uint32_t) * 6 + sizeof(uint64_t) * n_idx);
@@ -326,11 +362,19 @@ hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indic
     const uint32_t* dtab = static_cast<const uint32_t*>(tab.dev);
     const uint32_t m = n_idx + 1;
     const uint32_t need = mode == 0 ? m : n_idx;
-    if (need <= 8) return reveal_launch<8>(mode, a, B, n_idx, k, dtab, M, s);
-    if (need <= 16) return reveal_launch<16>(mode, a, B, n_idx, k, dtab, M, s);
-    if (need <= 32) return reveal_launch<32>(mode, a, B, n_idx, k, dtab, M, s);
-    if (need <= 64) return reveal_launch<64>(mode, a, B, n_idx, k, dtab, M, s);
-    return hipErrorInvalidValue;
+    unsigned int* log = static_cast<unsigned int*>(log_buf);
+    hipError_t e = hipSuccess;
+    if (mode == 0 && (e = hipMemsetAsync(log, 0, sizeof(unsigned int), s)) != hipSuccess) return e;
+    if (need <= 8) e = reveal_launch<8>(mode, a, B, n_idx, k, dtab, M, log, s);
+    else if (need <= 16) e = reveal_launch<16>(mode, a, B, n_idx, k, dtab, M, log, s);
+    else if (need <= 32) e = reveal_launch<32>(mode, a, B, n_idx, k, dtab, M, log, s);
+    else if (need <= 64) e = reveal_launch<64>(mode, a, B, n_idx, k, dtab, M, log, s);
+    else if (need <= kRevealMaxPoints) e = reveal_launch<kRevealMaxPoints>(mode, a, B, n_idx, k, dtab, M, log, s);
+    else return hipErrorInvalidValue;
+    if (e != hipSuccess || mode != 0) return e;
+    hipLaunchKernelGGL(packed_reveal_fixup_kernel, dim3(256), dim3(256), 0, s, a.shares, B, a.dimension, a.n_vectors,
+                       a.out, n_idx, k, dtab, p, log);
+    return hipGetLastError();
 }
 
 #endif  // SDA_REVEAL_PART

@@ -1,0 +1,90 @@
+"""GPU: the C ABI from a plain C program, with no torch and no Python in its process.
+
+tests/abi_c/full_loop.c links libsda_engine.so and the ROCm runtime it was built against
+(/opt/rocm/lib/libamdhip64), which is how the Rust FFI shim of INTEGRATION.md would bind it; every
+other GPU test reaches the engine through ctypes inside a torch process (whose bundled HIP runtime
+then serves the engine too).  It runs the four integration-tests/tests/full_loop.rs:30-150 variants
+with the golden fixture's draws and must reproduce every stage of the golden trace and
+`[2, 4, 6, 8]` (full_loop.rs:148).
+
+This module sorts before the other GPU test modules, so the subprocesses start before this pytest
+process has touched the GPU.
+"""
+import json
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BIN = os.path.join(HERE, "abi_c", "full_loop")
+
+KIND_MASK = {"None": 0, "Full": 1, "ChaCha": 2}
+
+
+def _program_input(v):
+    (mk, mp), = v["masking"].items() if isinstance(v["masking"], dict) else (("None", {}),)
+    (sk, sp), = v["sharing"].items()
+    lines = [f"{KIND_MASK[mk]} {mp.get('modulus', 0)} {mp.get('dimension', 0)} {mp.get('seed_bitsize', 0)}"]
+    if sk == "Additive":
+        lines.append(f"0 {sp['share_count']} {sp['modulus']} 1 {sp['share_count'] - 1} 0 0")
+    else:
+        lines.append(f"1 {sp['share_count']} {sp['prime_modulus']} {sp['secret_count']} {sp['privacy_threshold']} "
+                     f"{sp['omega_secrets']} {sp['omega_shares']}")
+    t = v["trace"]
+    D = len(v["inputs"][0])
+    lines.append(f"{D} 433 {len(v['inputs'])}")
+    for p, secrets in enumerate(v["inputs"]):
+        masks = t["masks"][p] if mk != "None" else []
+        lines.append(" ".join(map(str, secrets)))
+        lines.append(" ".join(map(str, [len(masks)] + masks)))
+        lines.append(" ".join(map(str, [len(t["draws"][p])] + t["draws"][p])))
+    n = len(t["clerk_results"])
+    lines.append(" ".join(map(str, [n] + list(range(n)))))
+    return "\n".join(lines) + "\n"
+
+
+def _parse(out):
+    res = {}
+    for line in out.splitlines():
+        if ":" in line:
+            k, v = line.split(":", 1)
+            res[k.strip()] = [int(x) for x in v.split()]
+    return res
+
+
+def _ensure_built():
+    if not os.path.exists(BIN):
+        subprocess.run(["make", "-C", os.path.dirname(BIN)], check=True, capture_output=True)
+
+
+@pytest.mark.parametrize("variant", ["simple", "with_fullmask", "with_chachamask", "with_packedshamir"])
+def test_c_program_full_loop(variant):
+    with open(os.path.join(HERE, "golden", "full_loop_kat.json")) as f:
+        v = json.load(f)[variant]
+    _ensure_built()
+    env = {k: val for k, val in os.environ.items() if not k.startswith("PYTHON")}
+    r = subprocess.run([BIN], input=_program_input(v), capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    got, t = _parse(r.stdout), v["trace"]
+    for p in range(len(v["inputs"])):
+        assert got[f"masks {p}"] == t["masks"][p]
+        assert got[f"masked {p}"] == t["masked"][p]
+        for c, row in enumerate(t["shares"][p]):
+            assert got[f"shares {p} {c}"] == row
+    for c, row in enumerate(t["clerk_results"]):
+        assert got[f"clerk {c}"] == row
+    if t["combined_mask"] is not None:
+        assert got["combined_mask"] == t["combined_mask"]
+    assert got["masked_output"] == t["masked_output"]
+    assert got["output"] == t["output"]
+    assert got["positive"] == [2, 4, 6, 8] == got["fused_reveal"]        # full_loop.rs:148
+
+
+def test_c_program_does_not_load_torch():
+    """The C consumer's process maps /opt/rocm's HIP runtime and no torch library."""
+    _ensure_built()
+    r = subprocess.run(["ldd", BIN], capture_output=True, text=True, timeout=60)
+    assert "libsda_engine.so" in r.stdout and "/opt/rocm" in r.stdout and "torch" not in r.stdout

@@ -206,10 +206,7 @@ def test_packed_generate_random(engine, oracle, sch):
 @pytest.mark.parametrize("sch", packed_schemes(), ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")
 def test_packed_reconstruct_random(engine, oracle, sch):
     p, n = sch.prime_modulus, sch.share_count
-    if n > 63:
-        n_max = 63
-    else:
-        n_max = n
+    n_max = n                      # batched.rs:75 uses every supplied share: up to all n clerks
     rng = np.random.default_rng(p % 777 + n)
     D = 23 * sch.secret_count + 1
     B = (D + sch.secret_count - 1) // sch.secret_count
@@ -217,8 +214,8 @@ def test_packed_reconstruct_random(engine, oracle, sch):
     draws = rng.integers(0, p - 1, size=B * sch.privacy_threshold(), dtype=np.int64)
     shares = oracle.packed_generate(_pp(oracle, sch), secrets, draws)
     need = sch.reconstruction_threshold()
-    for trial in range(4):
-        size = int(rng.integers(need, n_max + 1))
+    for trial in range(5):
+        size = n_max if trial == 0 else int(rng.integers(need, n_max + 1))
         idx = rng.permutation(n)[:size].tolist()
         got = engine.secret_reconstruct(sch, D, [(i, shares[i]) for i in idx])
         rc, exp = oracle.packed_reconstruct(_pp(oracle, sch), D, idx, shares[idx])
@@ -247,7 +244,10 @@ def test_packed_errors(engine):
 
 
 # ------------------------------------------------------------------ masking (north-star kernel 3)
-@pytest.mark.parametrize("m", [433, 2147482801, (1 << 40) + 7, (1 << 62) + 1])
+# (1 << 62) + 1: ~25 % of draws rejected; 0x5555555555555556: ~33 % rejected and, above 2^62, the
+# reference's `result[i] += m` wraps i64 (chacha.rs:70), so the combine is signed and order
+# dependent; I64_MAX: wrapping with almost no rejections
+@pytest.mark.parametrize("m", [433, 2147482801, (1 << 40) + 7, (1 << 62) + 1, 0x5555555555555556, I64_MAX])
 @pytest.mark.parametrize("words", [0, 1, 4, 8, 10])
 def test_chacha_mask_and_combine(engine, oracle, m, words):
     rng = np.random.default_rng(m % 991 + words)
@@ -263,6 +263,18 @@ def test_chacha_mask_and_combine(engine, oracle, m, words):
     got = engine.mask_combine(sch, rows)
     exp = oracle.chacha_mask_combine(m, D, np.stack(rows) if words else np.zeros((5, 0), np.int64))
     assert_same(got, exp)
+
+
+def test_chacha_wrapping_moduli_many_seeds(engine, oracle):
+    """m > 2^62: 40 seeds, so the running i64 sum wraps often; bit-exact with the reference's
+    sequential recurrence (the engine walks the seeds in order on its exact stream path)."""
+    rng = np.random.default_rng(62)
+    for m in (0x5555555555555556, I64_MAX - 24):
+        rows = [rng.integers(0, 2**32, size=4, dtype=np.uint64).astype(np.int64) for _ in range(40)]
+        got = engine.mask_combine(S.ChaChaMasking(m, 513, 128), rows)
+        exp = oracle.chacha_mask_combine(m, 513, np.stack(rows))
+        assert_same(got, exp)
+        assert (exp < 0).any()            # the wrap did happen
 
 
 def test_chacha_many_seeds(engine, oracle):

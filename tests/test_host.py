@@ -47,57 +47,71 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _run_world2(target):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+def _worker_rows(rank, world, port, q):
+    """sda_amd.distributed.combine_rows_sharded / combine_tiles_sharded themselves (participation
+    split, int64 all-reduce, finalize) with the oracle as the per-rank compute (tests/cpu_engine)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle as O
+    from tests.cpu_engine import CpuEngine
+    eng = CpuEngine()
     m, N, D = 2147482801, 37, 129
-    full = synth.fill(N, D, 0x5DA + 4, 0, m)             # non-negative inputs (configs[3])
+    full = torch.from_numpy(synth.fill(N, D, 0x5DA + 4, 0, m))      # non-negative inputs (configs[3])
     start, count = Dd.shard_range(N, rank, world)
-    part = torch.from_numpy(O.combine(m, full[start:start + count]))   # per-rank exact combine (CPU stand-in)
-    dist.all_reduce(part, op=dist.ReduceOp.SUM)          # int64 sum == u64 two's-complement sum
-    got = part.numpy() % m
+    mine = full[start:start + count].contiguous()
+    part, out = torch.empty(D, dtype=torch.int64), torch.empty(D, dtype=torch.int64)
+    Dd.combine_rows_sharded(eng, m, mine.data_ptr(), count, D, D, part, out)
+    res = {"rows": (out.tolist(), O.combine(m, full.numpy()).tolist())}
+    # the same rows streamed as 5-row tiles (configs[3]'s tiled accumulate on each rank)
+    tiles = [(mine[t0].data_ptr(), min(5, count - t0)) for t0 in range(0, count, 5)]
+    Dd.combine_tiles_sharded(eng, m, tiles, D, D, part, out)
+    res["tiles"] = (out.tolist(), res["rows"][1])
+    res["calls"] = sorted(set(eng.calls))
     if rank == 0:
-        q.put((got.tolist(), O.combine(m, full).tolist()))
+        q.put(res)
     dist.destroy_process_group()
 
 
 def test_gloo_world2_sharded_combine_matches_single_pass():
-    """The N-split + int64 all-reduce + final mod of sda_amd.distributed equals the reference's
-    single sequential pass for non-negative inputs (world size 2, gloo on CPU)."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    got, exp = q.get(timeout=120)
-    for p in procs:
-        p.join(timeout=60)
-    assert got == exp
+    """combine_rows_sharded and combine_tiles_sharded at world size 2 (gloo) equal the reference's
+    single sequential pass (combiner.rs:16-28) for non-negative inputs."""
+    res = _run_world2(_worker_rows)
+    assert res["rows"][0] == res["rows"][1]
+    assert res["tiles"][0] == res["tiles"][1]
+    assert res["calls"] == ["combine_accumulate_dev", "combine_dev", "combine_finalize_dev"]
 
 
-def _worker2(rank, world, port, q):
-    """reduce_canonical over the ChaCha mask N-split, and the column split of a signed combine,
-    with the oracle as the per-rank compute stand-in."""
+def _worker_mask_columns(rank, world, port, q):
+    """mask_combine_sharded (seed split + reduce) and combine_columns_sharded (signed column split +
+    all-gather), the product functions, with the oracle as the per-rank compute."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle as O
+    from tests.cpu_engine import CpuEngine
+    eng = CpuEngine()
     m, D = 2147482801, 301
     seeds = (np.arange(10 * 4, dtype=np.int64).reshape(10, 4) * 7919) % (1 << 31)
     s0, c = Dd.shard_range(10, rank, world)
-    part = torch.from_numpy(O.chacha_mask_combine(m, D, seeds[s0:s0 + c]))
-    out = torch.empty(D, dtype=torch.int64)
-    Dd.reduce_canonical(part, m, lambda p, o: o.copy_(torch.remainder(p, m)), out)
+    mine = torch.from_numpy(seeds[s0:s0 + c].astype(np.int32))
+    part, out = torch.empty(D, dtype=torch.int64), torch.empty(D, dtype=torch.int64)
+    Dd.mask_combine_sharded(eng, m, D, mine, part, out)
     res = {"mask": (out.tolist(), O.chacha_mask_combine(m, D, seeds).tolist())}
     x = synth.fill(23, D, 0x5DA + 9, -(m - 1), m)         # signed: order-dependent exact result
-    lo, cnt = Dd.column_slice(D, rank, world)
-    width = max(Dd.column_slice(D, r, world)[1] for r in range(world))
-    mine = torch.zeros(width, dtype=torch.int64)
-    mine[:cnt] = torch.from_numpy(O.combine(m, np.ascontiguousarray(x[:, lo:lo + cnt])))
-    parts = [torch.empty_like(mine) for _ in range(world)]
-    dist.all_gather(parts, mine)
-    full = torch.cat([parts[r][:Dd.column_slice(D, r, world)[1]] for r in range(world)])
+    full = torch.empty(D, dtype=torch.int64)
+    Dd.combine_columns_sharded(eng, m, torch.from_numpy(x), full)
     res["columns"] = (full.tolist(), O.combine(m, x).tolist())
     if rank == 0:
         q.put(res)
@@ -105,19 +119,23 @@ def _worker2(rank, world, port, q):
 
 
 def test_gloo_world2_mask_reduce_and_column_split():
-    """sda_amd.distributed: ChaCha mask combine split over seeds + reduce_canonical, and the signed
-    combine split over columns + all-gather, equal the single-pass reference (gloo, world 2)."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker2, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = q.get(timeout=120)
-    for p in procs:
-        p.join(timeout=60)
+    """sda_amd.distributed: ChaCha mask combine split over seeds + reduce, and the signed combine
+    split over columns + all-gather, equal the single-pass reference (gloo, world 2)."""
+    res = _run_world2(_worker_mask_columns)
     for k, (got, exp) in res.items():
         assert got == exp, k
+
+
+def test_world1_helpers_return_exact_signed_result():
+    """At world size 1 no reduce runs: the exact single-pass result is returned unchanged, signed
+    values included (no canonicalising finalize)."""
+    from oracle import oracle as O
+    from tests.cpu_engine import CpuEngine
+    m, N, D = 433, 9, 50
+    x = torch.from_numpy(synth.fill(N, D, 0x5DA + 3, -(m - 1), m))
+    part, out = torch.empty(D, dtype=torch.int64), torch.empty(D, dtype=torch.int64)
+    Dd.combine_rows_sharded(CpuEngine(), m, x.data_ptr(), N, D, D, part, out)
+    assert out.tolist() == O.combine(m, x.numpy()).tolist() and min(out.tolist()) < 0
 
 
 @pytest.mark.parametrize("dim,world", [(1, 2), (7, 3), (1000, 8), (5, 8)])
