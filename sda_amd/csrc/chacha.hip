@@ -65,19 +65,24 @@ struct RejectLog {
 // LAZY (m <= 2^32): the raw 64-bit words v are summed into 96-bit accumulators (3 adds per draw)
 // and reduced once per chunk -- (sum of v) mod m == sum of (v mod m) mod m; otherwise each draw
 // is reduced with the 64-bit Barrett `%`.
-template <bool LAZY>
-__global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __restrict__ seeds, uint32_t w,
-                                                             uint64_t n_seeds, uint64_t seeds_per_chunk,
-                                                             uint64_t D, unsigned long long* __restrict__ acc,
-                                                             Mod64 M, uint64_t zone, uint64_t r64, RejectLog log) {
-    const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// A lane owns elements 8 blk .. 8 blk + 7; the workgroup's 2048 results go through LDS so that the
+// write-back is coalesced (lane t writes element t + 256 j): plain stores when the grid has a
+// single seed chunk (DIRECT: acc is the output), atomics into acc otherwise.
+constexpr int kChachaPad = 9;                  // LDS row stride (u64) of a lane's 8 results
+template <bool LAZY, bool DIRECT>
+__global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __restrict__ seeds, uint32_t w, uint64_t n_seeds,
+                           uint64_t seeds_per_chunk, uint64_t D, unsigned long long* __restrict__ acc, Mod64 M,
+                           uint64_t zone, uint64_t r64, RejectLog log) {
+    __shared__ unsigned long long st[256 * kChachaPad];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + tid;
     const uint64_t n_blk = (D + 7) / 8;
-    if (blk >= n_blk) return;
+    const bool live = blk < n_blk;
     const uint64_t s0 = (uint64_t)blockIdx.y * seeds_per_chunk;
-    const uint64_t s1 = s0 + seeds_per_chunk < n_seeds ? s0 + seeds_per_chunk : n_seeds;
+    const uint64_t s1 = live ? (s0 + seeds_per_chunk < n_seeds ? s0 + seeds_per_chunk : n_seeds) : s0;
     const uint32_t nw = w < 8 ? w : 8;
     const uint64_t m = M.m;
-    const uint32_t nvalid = D - blk * 8 < 8 ? (uint32_t)(D - blk * 8) : 8u;   // pairs of this block inside D
+    const uint32_t nvalid = !live ? 0u : (D - blk * 8 < 8 ? (uint32_t)(D - blk * 8) : 8u);   // pairs inside D
     uint64_t a[8];
     uint32_t hi[8];
 #pragma unroll
@@ -109,14 +114,25 @@ __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __r
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        if ((uint32_t)q >= nvalid) continue;
         uint64_t r = a[q];
         if constexpr (LAZY) {       // (hi 2^64 + lo) mod m, m <= 2^32: hi mod m < m, r64 = 2^64 mod m
             const uint64_t t = umod64((uint64_t)hi[q], M) * r64;          // < m^2 <= 2^64
             const uint64_t x = umod64(t, M) + umod64(r, M);               // < 2m
             r = x >= m ? x - m : x;
         }
-        atomicAdd(&acc[blk * 8 + q], (unsigned long long)r);
+        st[tid * kChachaPad + q] = r;
+    }
+    __syncthreads();
+    const uint64_t e0 = (uint64_t)blockIdx.x * 2048;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t idx = j * 256 + tid;
+        const uint64_t e = e0 + idx;
+        if (e < D) {
+            const unsigned long long r = st[(idx >> 3) * kChachaPad + (idx & 7)];
+            if constexpr (DIRECT) acc[e] = r;
+            else atomicAdd(&acc[e], r);
+        }
     }
 }
 
@@ -389,28 +405,59 @@ static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_
     uint64_t* pair_of = reinterpret_cast<uint64_t*>(base + D * 8 + 16 + kRejectCap * 4);
     uint64_t* rej_up = pair_of + kRejectCap;
     hipError_t e;
-    if ((e = hipMemsetAsync(acc, 0, D * 8 + 16, s)) != hipSuccess) return e;
-
     const uint64_t n_blk = (D + 7) / 8;
     const uint64_t gx = (n_blk + 255) / 256;
-    // enough workgroups to fill 256 CUs x 8 waves; split seeds over grid.y
-    uint64_t chunks = (2048 + gx - 1) / gx;
-    if (chunks > n_seeds) chunks = n_seeds ? n_seeds : 1;
-    if (chunks > 65535) chunks = 65535;
-    // headroom: the u64 accumulators receive one canonical partial (< m) per chunk
-    if (M.m > 1 && chunks > UINT64_MAX / (M.m - 1)) chunks = UINT64_MAX / (M.m - 1);
-    const uint64_t per = n_seeds ? (n_seeds + chunks - 1) / chunks : 0;
-    RejectLog log{count, seed_of, pair_of, kRejectCap};
-    if (n_seeds) {
-        const uint64_t mm = (uint64_t)modulus;
-        if (mm <= (1ull << 32)) {
-            const uint64_t r64 = (UINT64_MAX % mm + 1) % mm;          // 2^64 mod m
-            hipLaunchKernelGGL(chacha_combine_kernel<true>, dim3((unsigned)gx, (unsigned)chunks), dim3(256), 0, s,
-                               seeds_dev, w, n_seeds, per, D, acc, M, zone, r64, log);
-        } else {
-            hipLaunchKernelGGL(chacha_combine_kernel<false>, dim3((unsigned)gx, (unsigned)chunks), dim3(256), 0, s,
-                               seeds_dev, w, n_seeds, per, D, acc, M, zone, (uint64_t)0, log);
+    const uint64_t mm = (uint64_t)modulus;
+    const bool lazy = mm <= (1ull << 32);
+    // Seeds split over grid.y chunks so that the grid fills the chip in whole rounds of resident
+    // workgroups: minimise rounds(C) x seeds-per-chunk(C).  The u64 accumulators receive one
+    // canonical partial (< m) per chunk (headroom).
+    static int cap_wgs = 0;
+    if (cap_wgs == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chacha_combine_kernel<true, false>, 256, 0);
+        // the API can be one block per CU high at 81-96 SGPRs (MI355X_MICROARCH.md): also bound it by
+        // the VGPR allocation (8-register granule, 512 per SIMD lane, 4 waves per block of 256)
+        hipFuncAttributes fa{};
+        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(chacha_combine_kernel<true, false>)) == hipSuccess &&
+            fa.numRegs > 0) {
+            const int by_vgpr = 512 / (((fa.numRegs + 7) / 8) * 8);
+            if (by_vgpr < per_cu) per_cu = by_vgpr;
         }
+        cap_wgs = (cus > 0 && per_cu > 0) ? cus * per_cu : 2048;
+    }
+    uint64_t max_c = n_seeds ? n_seeds : 1;
+    if (max_c > 4096) max_c = 4096;
+    if (M.m > 1 && max_c > UINT64_MAX / (M.m - 1)) max_c = UINT64_MAX / (M.m - 1);
+    uint64_t chunks = 1, best = UINT64_MAX;
+    for (uint64_t c = 1; c <= max_c; ++c) {
+        const uint64_t per_c = (n_seeds + c - 1) / c;
+        const uint64_t cost = ((gx * c + cap_wgs - 1) / cap_wgs) * (per_c ? per_c : 1);
+        if (cost < best) { best = cost; chunks = c; }
+    }
+    const uint64_t per = n_seeds ? (n_seeds + chunks - 1) / chunks : 0;
+    const bool direct = chunks == 1;             // results stored straight into `out`
+    unsigned long long* dst = direct ? reinterpret_cast<unsigned long long*>(out) : acc;
+    if ((e = hipMemsetAsync(count, 0, 16, s)) != hipSuccess) return e;
+    if (!direct && (e = hipMemsetAsync(acc, 0, D * 8, s)) != hipSuccess) return e;
+    RejectLog log{count, seed_of, pair_of, kRejectCap};
+    {
+        const dim3 grid((unsigned)gx, (unsigned)chunks);
+        const uint64_t r64 = lazy ? (UINT64_MAX % mm + 1) % mm : 0;          // 2^64 mod m
+        if (lazy && direct)
+            hipLaunchKernelGGL((chacha_combine_kernel<true, true>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per, D,
+                               dst, M, zone, r64, log);
+        else if (lazy)
+            hipLaunchKernelGGL((chacha_combine_kernel<true, false>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per,
+                               D, dst, M, zone, r64, log);
+        else if (direct)
+            hipLaunchKernelGGL((chacha_combine_kernel<false, true>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per,
+                               D, dst, M, zone, r64, log);
+        else
+            hipLaunchKernelGGL((chacha_combine_kernel<false, false>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per,
+                               D, dst, M, zone, r64, log);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         // read the rejection log (a few bytes) -- the call is synchronous anyway
         unsigned long long n_rej = 0;
@@ -421,10 +468,12 @@ static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_
             return hipSuccess;
         }
         if (n_rej) {
-            // canonicalise in place so the fix-ups can work modulo m without overflow
-            hipLaunchKernelGGL(acc_mod_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, acc, D,
-                               reinterpret_cast<int64_t*>(acc), M);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
+            // canonicalise in place so the fix-ups can work modulo m without overflow (DIRECT: already)
+            if (!direct) {
+                hipLaunchKernelGGL(acc_mod_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, acc, D,
+                                   reinterpret_cast<int64_t*>(acc), M);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+            }
             std::vector<uint32_t> so(n_rej);
             std::vector<uint64_t> po(n_rej);
             std::vector<uint32_t> seeds_host((size_t)n_seeds * w);     // only now: keys of the affected streams
@@ -458,13 +507,14 @@ static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_
                 const uint64_t i0 = rej.front();
                 const uint64_t nfix = D - i0;
                 hipLaunchKernelGGL(chacha_fix_kernel, dim3((unsigned)((nfix + 255) / 256)), dim3(256), 0, s, key, i0, D,
-                                   rej_up, (uint32_t)rej.size(), acc, M);
+                                   rej_up, (uint32_t)rej.size(), dst, M);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;   // rej_up is reused
                 if (fixups_out) ++*fixups_out;
             }
         }
     }
+    if (direct) return hipSuccess;
     hipLaunchKernelGGL(acc_mod_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, acc, D, out, M);
     return hipGetLastError();
 }

@@ -127,6 +127,8 @@ inline GenTables make_gen_tables(uint32_t L, uint32_t N3, int64_t p, int64_t ws,
 template <bool LAZY>
 struct Trunc {
     int32_t smin = 0x7FFFFFFF;
+    int32_t pend = 0;             // note1: values are folded into smin two at a time (one v_min3)
+    bool has_pend = false;        // (constant at every point of the unrolled code)
     __device__ __forceinline__ int32_t operator()(uint32_t c, uint32_t sw, uint32_t p) {
         if constexpr (LAZY) {
             return (int32_t)(c - (p & (uint32_t)((int32_t)sw >> 31)));
@@ -135,11 +137,13 @@ struct Trunc {
     }
     __device__ __forceinline__ void note1(int32_t a) {
         if constexpr (LAZY) {
-#if SDA_TRAP_ASM
-            asm("v_min_i32 %0, %0, %1" : "+v"(smin) : "v"(a));
-#else
-            smin = min(smin, a);
-#endif
+            if (has_pend) {
+                note2(pend, a);
+                has_pend = false;
+            } else {
+                pend = a;
+                has_pend = true;
+            }
         }
     }
     __device__ __forceinline__ void note2(int32_t a, int32_t b) {
@@ -152,7 +156,14 @@ struct Trunc {
         }
     }
     static constexpr bool lazy = LAZY;
-    __device__ __forceinline__ bool bad(uint32_t p) const { return LAZY && smin == -(int32_t)p; }
+    __device__ __forceinline__ bool bad(uint32_t p) {
+        if constexpr (LAZY) {
+            if (has_pend) note2(pend, pend);
+            has_pend = false;
+            return smin == -(int32_t)p;
+        }
+        return false;
+    }
 };
 
 // Montgomery product with a uniform (SGPR) multiplier as a fixed instruction sequence:

@@ -336,7 +336,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                         });
                         y[g + i] = r[0]; y[g + i + th] = r[1]; y[g + i + 2 * th] = r[2];
                         tr.note2(r[0].s, r[1].s);
-                        tr.note2(r[2].s, r[2].s);
+                        tr.note1(r[2].s);
                     }
                 });
             });

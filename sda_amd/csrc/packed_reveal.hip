@@ -46,18 +46,105 @@ __device__ __forceinline__ void reveal_flush(int64_t* lds_o, int64_t* o, uint64_
     }
 }
 
+// gather [clerk][batch] -> [clerk] (batched.rs:83-85); point 1 carries value 0.  Clamped,
+// branch-free indices, so every load can be issued before the first wait; each share is turned into
+// its (sign, residue) pair as it lands, so no i64 copy stays live.  Returns whether every share lies
+// in (-p, p).
+template <int MMAX>
+__device__ __forceinline__ bool load_points(const int64_t* __restrict__ sh, uint64_t B, uint32_t m, uint32_t p,
+                                            FE (&s)[MMAX]) {
+    const int64_t P = (int64_t)p;
+    s[0] = FE{0, 0};
+    bool in_range = true;
+    static_for<1, MMAX>([&](auto i) {
+        const int64_t v = sh[(uint64_t)((uint32_t)i < m ? i - 1 : 0) * B];
+        in_range = in_range && ((uint32_t)i >= m || (uint64_t)(v + (P - 1)) < (uint64_t)(2 * P - 1));
+        const int32_t x = (uint32_t)i < m ? (int32_t)v : 0;
+        s[i] = FE{x, canon32(x, p)};
+    });
+    return in_range;
+}
+
+// tss reconstruct of one batch from its m points (shares in (-p, p)): Newton divided differences,
+// then newton_evaluate at omega_secrets^(e+1), e < k; secrets e < lim go to dst[e].  With LAZY
+// (lazy truncation, packed_common.h: Trunc) returns whether the -p trap fired, in which case dst
+// holds garbage and the caller reruns the batch with LAZY = false (tss' `%` verbatim).
 // KU > 0: the evaluation loop over the k <= KU secrets is unrolled (table offsets become
 // compile-time constants: merged scalar loads, no per-secret loop overhead).
-// LAZY (p >= kLazyTruncMinP): lazy truncation (packed_common.h: Trunc) with the -p trap; a lane
-// whose batch hit it recomputes the batch on the generic exact path.
-// FULL: the point count is exactly MMAX (n_idx + 1 == MMAX), so every `i < m` guard is a compile-time
-// constant: no per-step uniform branches, and the table rows load as merged s_load_dwordx16.
-//
-// A lane whose batch has a share outside (-p, p) (raw i64 input), or whose lazy truncation hit the
-// -p trap, logs the batch and stores garbage; packed_reveal_fixup_kernel, launched right after on the
-// same stream, recomputes those batches on the generic exact path.  Keeping the generic path out of
-// this kernel keeps it free of scratch (its 128-entry i64 array used to cost 1 KiB of scratch per
-// lane, which capped the number of resident waves).
+// FULL: m == MMAX, so every `i < m` guard is a compile-time constant: no per-step uniform branches,
+// and the table rows load as merged s_load_dwordx16.
+template <int MMAX, int KU, bool LAZY, bool FULL>
+__device__ __forceinline__ bool newton_reveal(FE (&s)[MMAX], uint32_t m, uint32_t k, const uint32_t* __restrict__ tab,
+                                              const MontP& M, int64_t* dst, uint32_t lim) {
+    const uint32_t p = M.p;
+    Trunc<LAZY> tr;
+    // numtheory::compute_newton_coefficients: for j in 1..m { for i in (j..m).rev() {
+    //   s[i] = (((s[i] - s[i-1]) % p) * inv(points[i] - points[i-j])) % p } }
+    // inv >= 0, so the product has the sign of the exact difference (or is 0).
+    auto newton_step = [&](auto i, uint32_t j) {
+        const uint32_t dc = s[i].c - s[i - 1].c + p;      // lazy: (0, 2p), REDC input < 2p^2 < pR
+        const int32_t sg = __builtin_elementwise_sub_sat(s[i].s, s[i - 1].s);
+        const uint32_t fc = montu<false>(tab[OFF_INVM + j * TS + i], dc, M);
+        s[i] = FE{tr(fc, (uint32_t)sg, p), fc};
+        tr.note1(s[i].s);
+    };
+    if constexpr (MMAX <= 16) {
+        // fully unrolled triangle: every table word is a compile-time offset (merged s_loads)
+        static_for<1, MMAX>([&](auto j) {
+            if (FULL || (uint32_t)j < m) {
+                static_for<0, MMAX - j>([&](auto ii) {
+                    constexpr int i = MMAX - 1 - ii;
+                    if (FULL || (uint32_t)i < m) newton_step(std::integral_constant<int, i>{}, (uint32_t)j);
+                });
+            }
+        });
+    } else {
+        // wide index sets: runtime j, unrolled i (uniform branches); keeps code size O(MMAX)
+        for (uint32_t j = 1; j < m; ++j) {
+            static_for<0, MMAX - 1>([&](auto ii) {
+                constexpr int i = MMAX - 1 - ii;
+                if ((uint32_t)i < m && (uint32_t)i >= j) newton_step(std::integral_constant<int, i>{}, j);
+            });
+        }
+    }
+    // LAZY: -(p if coefficient i is negative else 0), hoisted out of the e loop
+    uint32_t nsp[LAZY ? MMAX : 1];
+    if constexpr (LAZY) static_for<0, MMAX>([&](auto i) { nsp[i] = 0u - (p & (uint32_t)(s[i].s >> 31)); });
+    // numtheory::newton_evaluate at omega_secrets^(e+1): fold((a + (coef * np) % p) % p)
+    auto eval = [&](uint32_t e) {
+        const uint32_t* np = tab + OFF_NP + e * TS;
+        const uint32_t* npm = tab + OFF_NPM + e * TS;
+        FE acc{0, 0};
+        static_for<0, MMAX>([&](auto i) {
+            if (FULL || (uint32_t)i < m) {
+                const uint32_t tc = montu<false>(npm[i], s[i].c, M);
+                // sign of s * np (np != 0 mod p; s == 0 makes tc == 0, exact unless LAZY, whose trap
+                // then sends the batch to the rerun).  LAZY: tc - p [sgn(s) xor sgn(np)]: with both
+                // terms in {0, -p}, -(a xor b) == (-a) xor (-b), so it is one v_xad_u32 of the hoisted
+                // per-coefficient term and the uniform per-table-entry one.
+                int32_t ts;
+                if constexpr (LAZY) ts = (int32_t)((nsp[i] ^ (0u - (p & (uint32_t)((int32_t)np[i] >> 31)))) + tc);
+                else ts = tr(tc, (uint32_t)s[i].s ^ np[i], p);
+                const uint32_t ac = addm(acc.c, tc, p);
+                acc = FE{tr(ac, (uint32_t)__builtin_elementwise_add_sat(acc.s, ts), p), ac};
+                tr.note2(ts, acc.s);
+            }
+        });
+        if (e < lim) dst[e] = acc.s;                                                // batched.rs:94
+    };
+    if constexpr (KU > 0) {
+        static_for<0, KU>([&](auto e) { if ((uint32_t)e < k) eval((uint32_t)e); });
+    } else {
+        for (uint32_t e = 0; e < k; ++e) eval(e);
+    }
+    return tr.bad(p);
+}
+
+// One lane = one batch.  LAZY (p >= kLazyTruncMinP): lazy truncation with the -p trap.  A lane whose
+// batch hit the trap (probability ~1/p per value) or has a share outside (-p, p) (raw i64 input) logs
+// the batch and stores garbage; packed_reveal_fixup_kernel, launched right after on the same stream,
+// recomputes the logged batches (exact truncation in registers, or the generic i64 path).  Keeping
+// the generic path (a 128-entry i64 array per lane) out of this kernel keeps it free of scratch.
 template <int MMAX, bool STAGED, int KU, bool LAZY, bool FULL = false>
 __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t* __restrict__ shares, uint64_t B,
                                                                   uint64_t D, int64_t* __restrict__ out,
@@ -71,89 +158,70 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
     const uint64_t vec = blockIdx.y;
     const int64_t* sh = shares + vec * (uint64_t)n_idx * B + (live ? b : B - 1);
     int64_t* o = out + vec * D;
-    const uint32_t p = M.p;
-    const int64_t P = (int64_t)p;
     const uint32_t m = FULL ? (uint32_t)MMAX : n_idx + 1;
     int64_t* dst = STAGED ? lds_o + tid * k : o + b * k;
     const uint32_t lim = STAGED ? k : (b * k < D ? (uint32_t)(D - b * k < k ? D - b * k : k) : 0u);
 
-    // gather [clerk][batch] -> [clerk] (batched.rs:83-85); point 1 carries value 0.  Clamped,
-    // branch-free indices, so every load can be issued before the first wait; each share is turned
-    // into its (sign, residue) pair as it lands, so no i64 copy stays live.
     FE s[MMAX];
-    s[0] = FE{0, 0};
-    bool in_range = true;
-    static_for<1, MMAX>([&](auto i) {
-        const int64_t v = sh[(uint64_t)((uint32_t)i < m ? i - 1 : 0) * B];
-        in_range = in_range && ((uint32_t)i >= m || (uint64_t)(v + (P - 1)) < (uint64_t)(2 * P - 1));
-        const int32_t x = (uint32_t)i < m ? (int32_t)v : 0;
-        s[i] = FE{x, canon32(x, p)};
-    });
-    Trunc<LAZY> tr;
-    if (in_range) {
-        // numtheory::compute_newton_coefficients: for j in 1..m { for i in (j..m).rev() {
-        //   s[i] = (((s[i] - s[i-1]) % p) * inv(points[i] - points[i-j])) % p } }
-        // inv >= 0, so the product has the sign of the exact difference (or is 0).
-        auto newton_step = [&](auto i, uint32_t j) {
-            const uint32_t dc = s[i].c - s[i - 1].c + p;      // lazy: (0, 2p), REDC input < 2p^2 < pR
-            const int32_t sg = __builtin_elementwise_sub_sat(s[i].s, s[i - 1].s);
-            const uint32_t fc = montu<false>(tab[OFF_INVM + j * TS + i], dc, M);
-            s[i] = FE{tr(fc, (uint32_t)sg, p), fc};
-            tr.note1(s[i].s);
-        };
-        if constexpr (MMAX <= 16) {
-            // fully unrolled triangle: every table word is a compile-time offset (merged s_loads)
-            static_for<1, MMAX>([&](auto j) {
-                if ((uint32_t)j < m) {
-                    static_for<0, MMAX - j>([&](auto ii) {
-                        constexpr int i = MMAX - 1 - ii;
-                        if ((uint32_t)i < m) newton_step(std::integral_constant<int, i>{}, (uint32_t)j);
-                    });
-                }
-            });
-        } else {
-            // wide index sets: runtime j, unrolled i (uniform branches); keeps code size O(MMAX)
-            for (uint32_t j = 1; j < m; ++j) {
-                static_for<0, MMAX - 1>([&](auto ii) {
-                    constexpr int i = MMAX - 1 - ii;
-                    if ((uint32_t)i < m && (uint32_t)i >= j) newton_step(std::integral_constant<int, i>{}, j);
-                });
-            }
-        }
-        uint32_t sgm[MMAX];
-        static_for<0, MMAX>([&](auto i) { sgm[i] = (uint32_t)(s[i].s >> 31); });
-        // numtheory::newton_evaluate at omega_secrets^(e+1): fold((a + (coef * np) % p) % p)
-        auto eval = [&](uint32_t e) {
-            const uint32_t* np = tab + OFF_NP + e * TS;
-            const uint32_t* npm = tab + OFF_NPM + e * TS;
-            FE acc{0, 0};
-            static_for<0, MMAX>([&](auto i) {
-                if ((uint32_t)i < m) {
-                    const uint32_t tc = montu<false>(npm[i], s[i].c, M);
-                    // sign of s * np (np != 0 mod p; s == 0 makes tc == 0, exact unless LAZY, whose
-                    // trap then sends the batch to the generic path).  LAZY: p & (sgn(s) ^ sgn(np))
-                    // is one v_bitop3 with the per-coefficient sign masks hoisted out of the e loop.
-                    int32_t ts;
-                    if constexpr (LAZY) ts = (int32_t)(tc - (p & (sgm[i] ^ (uint32_t)((int32_t)np[i] >> 31))));
-                    else ts = tr(tc, (uint32_t)s[i].s ^ np[i], p);
-                    const uint32_t ac = addm(acc.c, tc, p);
-                    acc = FE{tr(ac, (uint32_t)__builtin_elementwise_add_sat(acc.s, ts), p), ac};
-                    tr.note2(ts, acc.s);
-                }
-            });
-            if (e < lim) dst[e] = acc.s;                                                // batched.rs:94
-        };
-        if constexpr (KU > 0) {
-            static_for<0, KU>([&](auto e) { if ((uint32_t)e < k) eval((uint32_t)e); });
-        } else {
-            for (uint32_t e = 0; e < k; ++e) eval(e);
-        }
-    }
-    if ((!in_range || tr.bad(p)) && live) {           // -> packed_reveal_fixup_kernel
+    const bool in_range = load_points<MMAX>(sh, B, m, M.p, s);
+    const bool redo = !in_range || newton_reveal<MMAX, KU, LAZY, FULL>(s, m, k, tab, M, dst, lim);
+    if (redo && live) {                                  // -> packed_reveal_fixup_kernel
         const uint32_t slot = atomicAdd(log, 1u);
         if (slot < kGenLogCap) reinterpret_cast<uint64_t*>(log + 16)[slot] = vec * B + b;
     }
     reveal_flush<STAGED>(lds_o, o, b0, B, D, k);
+}
+
+// Generic exact reveal of one batch (shares outside (-p, p)): tss' Newton divided differences and
+// evaluation with wrapping i64 arithmetic and truncated `%`, reading the batch's shares from global
+// memory.  Writes its first `lim` secrets to dst[0..lim).
+__device__ void reveal_exact_generic(const int64_t* __restrict__ sh, uint64_t B, uint32_t m, uint32_t k,
+                                     const uint32_t* __restrict__ tab, uint32_t p, int64_t* dst, uint32_t lim) {
+    const Mod64 P = make_mod64((int64_t)p);
+    int64_t s[TS];
+    s[0] = 0;
+    for (uint32_t i = 1; i < m; ++i) s[i] = sh[(uint64_t)(i - 1) * B];
+    for (uint32_t j = 1; j < m; ++j)
+        for (uint32_t i = m - 1; i >= j; --i) {
+            const int64_t cd = trem64(wsub(s[i], s[i - 1]), P);
+            s[i] = trem64(wmul(cd, (int64_t)tab[OFF_INV + j * TS + i]), P);
+        }
+    for (uint32_t e = 0; e < k && e < lim; ++e) {
+        int64_t acc = 0;
+        for (uint32_t i = 0; i < m; ++i) {
+            const int64_t np = (int64_t)(int32_t)tab[OFF_NP + e * TS + i];
+            acc = trem64(wadd(acc, trem64(wmul(s[i], np), P)), P);
+        }
+        dst[e] = acc;
+    }
+}
+
+// The batches packed_reveal_exact_kernel logged: in-range ones (lazy-truncation traps) rerun the
+// register path with tss' truncation verbatim; out-of-range ones take the generic i64 path.  If the
+// log overflowed, every batch of the launch is recomputed (correct and slow; only reachable with raw
+// i64 shares).  One wave per workgroup: a logged batch is rare, so few lanes are busy.
+template <int MMAX, int KU>
+__global__ __launch_bounds__(64) void packed_reveal_fixup_kernel(const int64_t* __restrict__ shares, uint64_t B,
+                                                                 uint64_t D, uint64_t n_vec, int64_t* __restrict__ out,
+                                                                 uint32_t n_idx, uint32_t k,
+                                                                 const uint32_t* __restrict__ tab, MontP M,
+                                                                 const unsigned int* __restrict__ log) {
+    const uint32_t n = *log;
+    if (n == 0) return;
+    const bool all = n > kGenLogCap;
+    const uint64_t total = all ? B * n_vec : (uint64_t)n;
+    const uint64_t* list = reinterpret_cast<const uint64_t*>(log + 16);
+    const uint32_t m = n_idx + 1;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t gb = all ? i : list[i];
+        const uint64_t vec = gb / B, b = gb - vec * B;
+        const uint32_t lim = b * k < D ? (uint32_t)(D - b * k < k ? D - b * k : k) : 0u;
+        const int64_t* sh = shares + vec * (uint64_t)n_idx * B + b;
+        int64_t* dst = out + vec * D + b * k;
+        FE s[MMAX];
+        if (load_points<MMAX>(sh, B, m, M.p, s)) newton_reveal<MMAX, KU, false, false>(s, m, k, tab, M, dst, lim);
+        else reveal_exact_generic(sh, B, m, k, tab, M.p, dst, lim);
+    }
 }
 
 template <int NMAX, bool STAGED>
@@ -233,6 +301,14 @@ hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32
             hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, false, 0, false>), grid, dim3(256), 0, s, a.shares,
                                B, a.dimension, a.out, n_idx, k, tab, M, log);
         }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if (MM <= 16 && k <= 8)
+            hipLaunchKernelGGL((packed_reveal_fixup_kernel<MM, MM <= 16 ? 8 : 0>), dim3(64), dim3(64), 0, s, a.shares,
+                               B, a.dimension, a.n_vectors, a.out, n_idx, k, tab, M, log);
+        else
+            hipLaunchKernelGGL((packed_reveal_fixup_kernel<MM, 0>), dim3(64), dim3(64), 0, s, a.shares, B,
+                               a.dimension, a.n_vectors, a.out, n_idx, k, tab, M, log);
     } else {
         if (staged)
             hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, true>), grid, dim3(256), lds, s, a.shares, B,
@@ -246,56 +322,7 @@ hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32
 template hipError_t reveal_launch<SDA_REVEAL_PART>(int, const PackedRevealArgs&, uint64_t, uint32_t, uint32_t,
                                                    const uint32_t*, const MontP&, unsigned int*, hipStream_t);
 
-#else  // dispatcher, host tables, generic fix-up
-
-namespace {
-
-// Generic exact reveal of one batch (shares outside (-p, p), or a lazy-truncation trap): tss'
-// Newton divided differences and evaluation with wrapping i64 arithmetic and truncated `%`, reading
-// the batch's shares from global memory.  Writes its first `lim` secrets to dst[0..lim).
-__device__ void reveal_exact_generic(const int64_t* __restrict__ sh, uint64_t B, uint32_t m, uint32_t k,
-                                     const uint32_t* __restrict__ tab, uint32_t p, int64_t* dst, uint32_t lim) {
-    const Mod64 P = make_mod64((int64_t)p);
-    int64_t s[TS];
-    s[0] = 0;
-    for (uint32_t i = 1; i < m; ++i) s[i] = sh[(uint64_t)(i - 1) * B];
-    for (uint32_t j = 1; j < m; ++j)
-        for (uint32_t i = m - 1; i >= j; --i) {
-            const int64_t cd = trem64(wsub(s[i], s[i - 1]), P);
-            s[i] = trem64(wmul(cd, (int64_t)tab[OFF_INV + j * TS + i]), P);
-        }
-    for (uint32_t e = 0; e < k && e < lim; ++e) {
-        int64_t acc = 0;
-        for (uint32_t i = 0; i < m; ++i) {
-            const int64_t np = (int64_t)(int32_t)tab[OFF_NP + e * TS + i];
-            acc = trem64(wadd(acc, trem64(wmul(s[i], np), P)), P);
-        }
-        dst[e] = acc;
-    }
-}
-
-// Batches the exact kernel logged, recomputed with the generic path.  If the log overflowed, every
-// batch of the launch is recomputed (correct and slow; only reachable with raw i64 shares).
-__global__ __launch_bounds__(256) void packed_reveal_fixup_kernel(const int64_t* __restrict__ shares, uint64_t B,
-                                                                  uint64_t D, uint64_t n_vec, int64_t* __restrict__ out,
-                                                                  uint32_t n_idx, uint32_t k,
-                                                                  const uint32_t* __restrict__ tab, uint32_t p,
-                                                                  const unsigned int* __restrict__ log) {
-    const uint32_t n = *log;
-    if (n == 0) return;
-    const bool all = n > kGenLogCap;
-    const uint64_t total = all ? B * n_vec : (uint64_t)n;
-    const uint64_t* list = reinterpret_cast<const uint64_t*>(log + 16);
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t gb = all ? i : list[i];
-        const uint64_t vec = gb / B, b = gb - vec * B;
-        const uint32_t lim = b * k < D ? (uint32_t)(D - b * k < k ? D - b * k : k) : 0u;
-        reveal_exact_generic(shares + vec * (uint64_t)n_idx * B + b, B, n_idx + 1, k, tab, p, out + vec * D + b * k,
-                             lim);
-    }
-}
-
-}  // namespace
+#else  // dispatcher + host tables
 
 // Host precompute of the per-index-set tables (data independent; same ops as tss).
 static void build_reveal_tables(std::vector<uint32_t>& tab, const uint64_t* indices, uint32_t n_idx, uint32_t k,
@@ -371,10 +398,7 @@ hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indic
     else if (need <= 64) e = reveal_launch<64>(mode, a, B, n_idx, k, dtab, M, log, s);
     else if (need <= kRevealMaxPoints) e = reveal_launch<kRevealMaxPoints>(mode, a, B, n_idx, k, dtab, M, log, s);
     else return hipErrorInvalidValue;
-    if (e != hipSuccess || mode != 0) return e;
-    hipLaunchKernelGGL(packed_reveal_fixup_kernel, dim3(256), dim3(256), 0, s, a.shares, B, a.dimension, a.n_vectors,
-                       a.out, n_idx, k, dtab, p, log);
-    return hipGetLastError();
+    return e;
 }
 
 #endif  // SDA_REVEAL_PART
