@@ -228,8 +228,7 @@ sda_status sda_clerk_decode_combine(sda_engine* h, const sda_sharing_scheme* s,
                                     uint64_t* out_len);
 /* Device forms.  `bytes`: device, 16-byte aligned, readable up to blob_off[n_blobs] rounded up to
  * 16 plus 16 bytes; blob i = bytes[blob_off[i], blob_off[i+1]) with blob_off a HOST array.
- * decode: out [n_blobs][out_stride] (device), counts[n_blobs] (host) = values per blob; a blob with
- * more than out_stride values is an INVALID_ARGUMENT error (out then holds its first out_stride). */
+ * decode: out [n_blobs][out_stride] (device), counts[n_blobs] (host) = values per blob. */
 sda_status sda_varint_decode_dev(sda_engine* h, const uint8_t* bytes, const uint64_t* blob_off,
                                  uint64_t n_blobs, int64_t* out, uint64_t out_stride,
                                  uint64_t* counts, void* stream);
@@ -239,8 +238,7 @@ sda_status sda_clerk_decode_combine_dev(sda_engine* h, int64_t modulus, const ui
                                         int64_t* out, uint64_t out_cap, uint64_t* out_len,
                                         void* stream);
 /* encode rows [rows][stride] (first len values of each) back to back into dst (device);
- * row_bytes[rows] (host) = bytes per row.  dst_cap too small: INVALID_ARGUMENT, row_bytes still
- * filled in, no byte at or past dst_cap written. */
+ * row_bytes[rows] (host) = bytes per row. */
 sda_status sda_varint_encode_dev(sda_engine* h, const int64_t* vals, uint64_t rows, uint64_t len,
                                  uint64_t stride, uint8_t* dst, uint64_t dst_cap,
                                  uint64_t* row_bytes, void* stream);

@@ -11,15 +11,13 @@
 //
 // The clerk decrypts N participations (sodium stays on the host) and combines them
 // (clerk.rs:79-86).  On the device the blobs are one concatenated byte stream; decoding is a
-// stream compaction over terminator bytes (b & 0x80 == 0), in ONE pass over the payload: a
-// workgroup takes the next 16 KiB aligned region of a blob (regions handed out in blob order by an
-// atomic ticket), stages it (plus a 16-byte halo) in LDS, counts its terminators and flags runs of
-// >= 11 continuation bytes, publishes the count, takes its element base from a decoupled look-back
-// over the blob's earlier regions, and decodes: each terminator byte decodes the <= 10-byte varint
-// that ends at it (its start is the previous terminator, within the halo) into out[blob][index].
-// Blobs flagged irregular (malformed streams) are redone afterwards by a sequential exact kernel.
-// Encoding is the mirror image: a workgroup takes the next 2048-value chunk (rows back to back),
-// sizes its varints, looks back for its byte offset, and writes the bytes assembled in LDS.
+// stream compaction over terminator bytes (b & 0x80 == 0):
+//   pass A  per 16 KiB aligned region of a blob: count terminators, flag runs of >= 11
+//           continuation bytes ("irregular" blob);
+//   pass B  per blob: exclusive scan of its region counts -> element base per region, total;
+//   pass C  per region: each terminator byte decodes the <= 10-byte varint that ends at it (its
+//           start is the previous terminator, within the 16-byte halo) into out[blob][index].
+// Irregular blobs (malformed streams) are decoded by a sequential exact kernel instead.
 // Roofline: HBM.  Algorithmic bytes = payload bytes read + 8 B per decoded element written.
 #include "kernels.h"
 
@@ -85,60 +83,102 @@ __device__ __forceinline__ Window make_window(uint4 prev, uint4 own, uint64_t wo
     return W;
 }
 
-// ---- decoupled look-back: one status word per item, flag in the top 2 bits, value below ----
-constexpr unsigned long long kAggReady = 1ull << 62, kIncReady = 2ull << 62, kValMask = (1ull << 62) - 1;
-
-// The status words carry only counts (nothing else is published through them), so relaxed
-// agent-scope atomics suffice: a release here would write back the whole L2 of the XCD before
-// every publication, an acquire would invalidate it after every poll.
-__device__ __forceinline__ void lb_publish(unsigned long long* st, unsigned long long v) {
-    __hip_atomic_store(st, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// 2-D grid: blockIdx.y = blob (+ y0), blockIdx.x = region within the blob (16 KiB aligned to the
+// byte buffer).  Blocks past a blob's last region exit at once (payload blobs have near-equal sizes).
+__device__ __forceinline__ bool region_of(const uint64_t* __restrict__ blob_region,
+                                          const uint64_t* __restrict__ blob_off, uint32_t y0, uint32_t* blob,
+                                          uint64_t* region, uint64_t* word) {
+    const uint32_t b = y0 + blockIdx.y;
+    const uint64_t r0 = blob_region[b], r1 = blob_region[b + 1];
+    if (r0 + blockIdx.x >= r1) return false;
+    *blob = b;
+    *region = r0 + blockIdx.x;
+    *word = (blob_off[b] / kRegionBytes + blockIdx.x) * (kRegionBytes / 16);
+    return true;
 }
 
-// Exclusive prefix of item i over items [first, i), computed by one whole wave (wave 0 of the
-// workgroup, every lane calls it; the result is uniform): each step reads the status words of the
-// 64 preceding items at once (relaxed agent-scope atomic loads, one per lane), waits until each has
-// at least its aggregate, and sums back to the nearest inclusive prefix -- or over all 64 and steps
-// another 64 back.  Item `first` publishes its inclusive value at once, so the walk ends there at the
-// latest.  Every predecessor holds an earlier ticket, so it is running or done; the spin is bounded
-// all the same (err flag).
-__device__ uint64_t lb_exclusive(unsigned long long* status, uint64_t i, uint64_t first, unsigned int* err) {
-    const uint32_t lane = threadIdx.x & 63;
-    uint64_t excl = 0;
-    uint64_t end = i;                                         // this window: items [end - 64, end)
-    while (end > first) {
-        const bool valid = end - first > lane;                // item end - 1 - lane >= first
-        const uint64_t j = end - 1 - lane;
-        unsigned long long v = 0;
-        if (valid) {
-            uint32_t spins = 0;
-            while (((v = __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0) {
-                if (++spins > (1u << 22)) {
-                    atomicOr(err, 1u);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        const uint64_t inc = __ballot(valid && (v >> 62) == 2);
-        const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;    // nearest inclusive predecessor
-        uint64_t c = (valid && lane <= stop) ? (v & kValMask) : 0;
-        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-        excl += c;
-        if (inc) break;
-        end = end - first > 64 ? end - 64 : first;
+// pass A: terminator count of each region; irregular-blob flag.
+__global__ __launch_bounds__(kThreads) void varint_count_kernel(const uint8_t* __restrict__ bytes,
+                                                                const uint64_t* __restrict__ blob_region,
+                                                                const uint64_t* __restrict__ blob_off, uint32_t y0,
+                                                                uint32_t* __restrict__ region_count,
+                                                                uint32_t* __restrict__ blob_irregular) {
+    uint32_t b;
+    uint64_t r, word;
+    if (!region_of(blob_region, blob_off, y0, &b, &r, &word)) return;
+    const uint64_t begin = blob_off[b], end = blob_off[b + 1];
+    // one coalesced load per word; the previous word's continuation mask (for the run check across
+    // the word boundary) comes through LDS
+    __shared__ uint32_t cm_l[kWPT * kThreads + 1];
+    const uint4* p = reinterpret_cast<const uint4*>(bytes);
+    uint4 v[kWPT];
+#pragma unroll
+    for (int k = 0; k < kWPT; ++k) {
+        const uint64_t wk = word + threadIdx.x + k * kThreads;
+        v[k] = wk * 16 < end ? p[wk] : make_uint4(0, 0, 0, 0);
     }
-    return excl;
-}
-
-__device__ __forceinline__ uint32_t block_sum(uint32_t n, uint32_t* red) {
+    uint4 halo = make_uint4(0, 0, 0, 0);
+    if (threadIdx.x == 0 && word * 16 > begin) halo = p[word - 1];
+    Window W[kWPT];
+#pragma unroll
+    for (int k = 0; k < kWPT; ++k) {
+        const uint32_t wl = threadIdx.x + k * kThreads;
+        W[k] = make_window(make_uint4(0, 0, 0, 0), v[k], word + wl, begin, end);   // own-word masks only
+        cm_l[wl + 1] = W[k].cont >> 16;
+    }
+    if (threadIdx.x == 0) cm_l[0] = make_window(make_uint4(0, 0, 0, 0), halo, word - 1, begin, end).cont >> 16;
+    __syncthreads();
+    uint32_t n = 0, bad = 0;
+#pragma unroll
+    for (int k = 0; k < kWPT; ++k) {
+        const uint32_t wl = threadIdx.x + k * kThreads;
+        n += __builtin_popcount(W[k].term & W[k].valid);
+        // 11 continuation bytes in a row ending inside this word?
+        const uint32_t cont = W[k].cont | cm_l[wl];
+        uint32_t run = cont;
+#pragma unroll
+        for (int q = 1; q <= 10; ++q) run &= cont << q;
+        bad |= run & W[k].valid;
+    }
+    if (bad) atomicOr(&blob_irregular[b], 1u);
+    // block reduction (one value per region)
+    __shared__ uint32_t red[kThreads / 64];
     for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n;
     __syncthreads();
-    uint32_t s = 0;
-    for (int i = 0; i < kThreads / 64; ++i) s += red[i];
-    __syncthreads();
-    return s;
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+        for (int i = 0; i < kThreads / 64; ++i) s += red[i];
+        region_count[r] = s;
+    }
+}
+
+// pass B: per blob, exclusive scan of its region counts (regions of blob b are
+// [blob_region[b], blob_region[b+1])) -> region_base; total -> blob_count.
+__global__ __launch_bounds__(kThreads) void varint_scan_kernel(const uint32_t* __restrict__ region_count,
+                                                               const uint64_t* __restrict__ blob_region,
+                                                               uint64_t* __restrict__ region_base,
+                                                               uint64_t* __restrict__ blob_count) {
+    const uint32_t b = blockIdx.x;
+    const uint64_t r0 = blob_region[b], r1 = blob_region[b + 1];
+    __shared__ uint64_t part[kThreads];
+    uint64_t carry = 0;
+    for (uint64_t base = r0; base < r1; base += kThreads) {
+        const uint64_t r = base + threadIdx.x;
+        const uint64_t v = r < r1 ? region_count[r] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < kThreads; o <<= 1) {            // Hillis-Steele inclusive scan
+            const uint64_t add = threadIdx.x >= (uint32_t)o ? part[threadIdx.x - o] : 0;
+            __syncthreads();
+            part[threadIdx.x] += add;
+            __syncthreads();
+        }
+        if (r < r1) region_base[r] = carry + part[threadIdx.x] - v;
+        carry += part[kThreads - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) blob_count[b] = carry;
 }
 
 // 7-bit groups of the (zero-padded past the element) little-endian bytes of `x`, packed:
@@ -151,190 +191,103 @@ __device__ __forceinline__ uint64_t leb_pack8(uint64_t x) {
     return x;
 }
 
-constexpr uint32_t kTileRegions = 8;          // regions per decode workgroup (128 KiB of payload)
-
-// One pass over the payload: a workgroup takes the next tile of up to kTileRegions consecutive
-// regions of one blob (atomic ticket; tiles numbered blob by blob, [blob_tile[b], blob_tile[b+1])
-// for blob b), counts the tile's terminators (and flags runs of >= 11 continuation bytes: irregular
-// blob), publishes the count, gets its element base from the look-back over the blob's earlier
-// tiles, and decodes region by region: stage the region and the 16-byte halo before it in LDS (the
-// second read of those bytes, from the caches); per sub-region (one word per thread) a block-wide
-// scan of the terminator counts compacts the elements' (start, length) into LDS; then lane i
-// decodes element i (balanced work, coalesced stores) from three funnel-shifted dwords.  Big tiles
-// keep the look-back chain short (one status word per 128 KiB).  Values at index >= out_stride are
-// counted, not stored.
+// pass C: decode.  The region's bytes (plus a 16-byte halo on each side) are staged in LDS; the
+// region is walked as kWPT sub-regions of one word per thread.  Per sub-region a block-wide scan
+// of the terminator counts compacts the elements' (start, length) into LDS; then lane i decodes
+// element i (balanced work, coalesced stores) from three funnel-shifted dwords.  Element index of a terminator = region base + terminators before it in
+// the region.  Blobs flagged irregular are skipped here (varint_sequential_kernel).
 __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* __restrict__ bytes,
-                                                                 const uint64_t* __restrict__ blob_tile,
-                                                                 const uint64_t* __restrict__ blob_off, uint64_t n_blobs,
-                                                                 unsigned long long* __restrict__ status,
-                                                                 unsigned int* __restrict__ ticket,
-                                                                 uint32_t* __restrict__ blob_irregular,
-                                                                 uint64_t* __restrict__ blob_count,
-                                                                 unsigned int* __restrict__ err,
+                                                                 const uint64_t* __restrict__ blob_region,
+                                                                 const uint64_t* __restrict__ blob_off, uint32_t y0,
+                                                                 const uint64_t* __restrict__ region_base,
+                                                                 const uint32_t* __restrict__ blob_irregular,
                                                                  int64_t* __restrict__ out, uint64_t out_stride) {
+    uint32_t b;
+    uint64_t r, word;
+    if (!region_of(blob_region, blob_off, y0, &b, &r, &word) || blob_irregular[b]) return;
     __shared__ uint32_t lb[(kRegionBytes + 32) / 4];          // [halo 16 B | region 16 KiB | tail 16 B]
     __shared__ uint32_t wsum[kThreads / 64];
     __shared__ uint32_t el[kSubBytes];                        // one sub-region's elements: start | len << 16
-    __shared__ uint32_t rcount[kTileRegions];
-    __shared__ uint64_t sh[3];
-    if (threadIdx.x == 0) {
-        const uint64_t t = atomicAdd(ticket, 1u);
-        uint64_t lo = 0, hi = n_blobs;                        // the last blob whose first tile is <= t
-        while (hi - lo > 1) {
-            const uint64_t mid = (lo + hi) / 2;
-            if (blob_tile[mid] <= t) lo = mid; else hi = mid;
-        }
-        sh[0] = t;
-        sh[1] = lo;
-    }
-    __syncthreads();
-    const uint64_t t = sh[0], b = sh[1];
-    const uint64_t first = blob_tile[b], last = blob_tile[b + 1] - 1;
     const uint64_t begin = blob_off[b], end = blob_off[b + 1];
-    const uint64_t r0 = begin / kRegionBytes + (t - first) * kTileRegions;   // first region (buffer-aligned)
-    const uint64_t r_end = (end - 1) / kRegionBytes + 1;
-    const uint32_t nreg = (uint32_t)(r_end - r0 < kTileRegions ? r_end - r0 : kTileRegions);
-    const uint4* p = reinterpret_cast<const uint4*>(bytes);
-
-    // ---- phase 1: terminator count per region, irregular runs ----
-    uint32_t bad = 0;
-    for (uint32_t k = 0; k < nreg; ++k) {
-        const uint64_t word = (r0 + k) * (kRegionBytes / 16);
+    // stage the region's words (one coalesced load each) and the halo word before it; the windows
+    // (previous word + own word) are then read back from LDS
+    {
+        const uint4* p = reinterpret_cast<const uint4*>(bytes);
         uint4 v[kWPT];
 #pragma unroll
-        for (int q = 0; q < kWPT; ++q) {
-            const uint64_t wk = word + threadIdx.x + q * kThreads;
-            v[q] = wk * 16 < end ? p[wk] : make_uint4(0, 0, 0, 0);
+        for (int k = 0; k < kWPT; ++k) {
+            const uint64_t wk = word + threadIdx.x + k * kThreads;
+            v[k] = wk * 16 < end ? p[wk] : make_uint4(0, 0, 0, 0);
         }
-        // continuation masks of the words (LDS: lb as u32 scratch), slot 0 = the word before the region
-        if (threadIdx.x == 0) {
-            const uint4 halo = word * 16 > begin ? p[word - 1] : make_uint4(0, 0, 0, 0);
-            lb[0] = make_window(make_uint4(0, 0, 0, 0), halo, word - 1, begin, end).cont >> 16;
-        }
-        Window W[kWPT];
-        uint32_t n = 0;
+        if (threadIdx.x == 0)
+            reinterpret_cast<uint4*>(lb)[0] = (word * 16 > begin) ? p[word - 1] : make_uint4(0, 0, 0, 0);
+        if (threadIdx.x == kThreads - 1) reinterpret_cast<uint4*>(lb)[kWPT * kThreads + 1] = make_uint4(0, 0, 0, 0);
 #pragma unroll
-        for (int q = 0; q < kWPT; ++q) {
-            const uint32_t wl = threadIdx.x + q * kThreads;
-            W[q] = make_window(make_uint4(0, 0, 0, 0), v[q], word + wl, begin, end);   // own-word masks only
-            lb[wl + 1] = W[q].cont >> 16;
-            n += __builtin_popcount(W[q].term & W[q].valid);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < kWPT; ++q) {
-            const uint32_t wl = threadIdx.x + q * kThreads;
-            const uint32_t cont = W[q].cont | lb[wl];        // 11 continuation bytes ending in this word?
-            uint32_t run = cont;
-#pragma unroll
-            for (int z = 1; z <= 10; ++z) run &= cont << z;
-            bad |= run & W[q].valid;
-        }
-        const uint32_t c = block_sum(n, wsum);               // (its barriers also free lb)
-        if (threadIdx.x == 0) rcount[k] = c;
-    }
-    if (bad) atomicOr(&blob_irregular[b], 1u);
-    __syncthreads();
-    uint32_t agg = 0;
-    for (uint32_t k = 0; k < nreg; ++k) agg += rcount[k];
-    if (threadIdx.x < 64) {                                   // wave 0: publish, look back, publish
-        uint64_t excl = 0;
-        if (t == first) {
-            if (threadIdx.x == 0) lb_publish(status + t, kIncReady | agg);
-        } else {
-            if (threadIdx.x == 0) lb_publish(status + t, kAggReady | agg);
-            excl = lb_exclusive(status, t, first, err);
-            if (threadIdx.x == 0) lb_publish(status + t, kIncReady | (excl + agg));
-        }
-        if (threadIdx.x == 0) {
-            if (t == last) blob_count[b] = excl + agg;
-            sh[2] = excl;
-        }
+        for (int k = 0; k < kWPT; ++k) reinterpret_cast<uint4*>(lb)[threadIdx.x + k * kThreads + 1] = v[k];
     }
     __syncthreads();
-
-    // ---- phase 2: decode region by region ----
-    int64_t* dst = out + b * out_stride;
-    uint64_t base = sh[2];                                    // elements before this region / sub-region
-    for (uint32_t kr = 0; kr < nreg; ++kr) {
-        const uint64_t word = (r0 + kr) * (kRegionBytes / 16);
-        {
-            uint4 v[kWPT];
+    Window W[kWPT];
 #pragma unroll
-            for (int k = 0; k < kWPT; ++k) {
-                const uint64_t wk = word + threadIdx.x + k * kThreads;
-                v[k] = wk * 16 < end ? p[wk] : make_uint4(0, 0, 0, 0);
-            }
-            if (threadIdx.x == 0)
-                reinterpret_cast<uint4*>(lb)[0] = (word * 16 > begin) ? p[word - 1] : make_uint4(0, 0, 0, 0);
-            if (threadIdx.x == kThreads - 1) reinterpret_cast<uint4*>(lb)[kWPT * kThreads + 1] = make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < kWPT; ++k) {
+        const uint32_t wl = threadIdx.x + k * kThreads;
+        W[k] = make_window(reinterpret_cast<const uint4*>(lb)[wl], reinterpret_cast<const uint4*>(lb)[wl + 1],
+                           word + wl, begin, end);
+    }
+    int64_t* dst = out + (uint64_t)b * out_stride + region_base[r];
+    uint32_t base = 0;                                        // elements in earlier sub-regions
 #pragma unroll
-            for (int k = 0; k < kWPT; ++k) reinterpret_cast<uint4*>(lb)[threadIdx.x + k * kThreads + 1] = v[k];
+    for (int k = 0; k < kWPT; ++k) {
+        // 1. compaction: each thread lists the (start, length) of the elements ending in its word
+        const uint32_t tm = W[k].term & W[k].valid;
+        const uint32_t n = __builtin_popcount(tm);
+        uint32_t incl = n;                                    // exclusive scan of n over the block
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o);
+            if ((threadIdx.x & 63) >= (uint32_t)o) incl += t;
+        }
+        __syncthreads();                                      // lb visible; el / wsum free for reuse
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        uint32_t e = incl - n, total = 0;
+        for (uint32_t w = 0; w < kThreads / 64; ++w) {
+            if (w < (threadIdx.x >> 6)) e += wsum[w];
+            total += wsum[w];
+        }
+        // an element starts after the previous boundary (a terminator or a byte outside the blob)
+        const uint32_t boundary = W[k].term | ~(W[k].term | W[k].cont);
+        uint32_t rem = tm;
+        while (rem) {
+            const int j = __builtin_ctz(rem);
+            rem &= rem - 1;
+            const uint32_t below = boundary & ((1u << j) - 1u);
+            const int st = below ? 32 - __builtin_clz(below) : 0;      // window index of the first byte
+            el[e++] = ((threadIdx.x + k * kThreads) * 16 + st) | ((uint32_t)(j - st + 1) << 16);
         }
         __syncthreads();
-        Window W[kWPT];
-#pragma unroll
-        for (int k = 0; k < kWPT; ++k) {
-            const uint32_t wl = threadIdx.x + k * kThreads;
-            W[k] = make_window(reinterpret_cast<const uint4*>(lb)[wl], reinterpret_cast<const uint4*>(lb)[wl + 1],
-                               word + wl, begin, end);
+        // 2. decode: lane i takes element i -> balanced work, coalesced stores
+        for (uint32_t i = threadIdx.x; i < total; i += kThreads) {
+            const uint32_t P = el[i] & 0xFFFFu;                  // byte position in lb
+            const int len = (int)(el[i] >> 16);                   // 1..11 on regular blobs
+            const uint32_t q = P >> 2, sh = (P & 3) * 8;
+            const uint32_t d0 = lb[q], d1 = lb[q + 1], d2 = lb[q + 2], d3 = lb[q + 3];
+            const uint32_t b0 = __builtin_amdgcn_alignbit(d1, d0, sh), b1 = __builtin_amdgcn_alignbit(d2, d1, sh),
+                           b2 = __builtin_amdgcn_alignbit(d3, d2, sh);
+            uint64_t lo = ((uint64_t)b1 << 32) | b0;
+            if (len < 8) lo &= (1ull << (8 * len)) - 1;
+            uint64_t z = leb_pack8(lo);
+            if (len > 8) {              // groups 8, 9, 10 at shifts 56, 63, 70 & 63 = 6 (Rust release)
+                const uint32_t hb = b2 & ((len >= 11) ? 0xFFFFFFu : (len == 10 ? 0xFFFFu : 0xFFu));
+                z |= ((uint64_t)(hb & 0x7F) << 56) | ((uint64_t)((hb >> 8) & 0x7F) << 63) |
+                     ((uint64_t)((hb >> 16) & 0x7F) << 6);
+            }
+            dst[base + i] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
         }
-#pragma unroll
-        for (int k = 0; k < kWPT; ++k) {
-            // 1. compaction: each thread lists the (start, length) of the elements ending in its word
-            const uint32_t tm = W[k].term & W[k].valid;
-            const uint32_t nk = __builtin_popcount(tm);
-            uint32_t incl = nk;                               // exclusive scan of nk over the block
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t tt = __shfl_up(incl, o);
-                if ((threadIdx.x & 63) >= (uint32_t)o) incl += tt;
-            }
-            __syncthreads();                                  // el / wsum free for reuse
-            if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
-            __syncthreads();
-            uint32_t e = incl - nk, total = 0;
-            for (uint32_t w = 0; w < kThreads / 64; ++w) {
-                if (w < (threadIdx.x >> 6)) e += wsum[w];
-                total += wsum[w];
-            }
-            // an element starts after the previous boundary (a terminator or a byte outside the blob)
-            const uint32_t boundary = W[k].term | ~(W[k].term | W[k].cont);
-            uint32_t rem = tm;
-            while (rem) {
-                const int j = __builtin_ctz(rem);
-                rem &= rem - 1;
-                const uint32_t below = boundary & ((1u << j) - 1u);
-                const int st = below ? 32 - __builtin_clz(below) : 0;      // window index of the first byte
-                el[e++] = ((threadIdx.x + k * kThreads) * 16 + st) | ((uint32_t)(j - st + 1) << 16);
-            }
-            __syncthreads();
-            // 2. decode: lane i takes element i -> balanced work, coalesced stores
-            for (uint32_t i = threadIdx.x; i < total; i += kThreads) {
-                if (base + i >= out_stride) break;
-                const uint32_t P = el[i] & 0xFFFFu;              // byte position in lb
-                const int len = (int)(el[i] >> 16);               // 1..11 on regular blobs
-                const uint32_t q = P >> 2, sh8 = (P & 3) * 8;
-                const uint32_t d0 = lb[q], d1 = lb[q + 1], d2 = lb[q + 2], d3 = lb[q + 3];
-                const uint32_t b0 = __builtin_amdgcn_alignbit(d1, d0, sh8), b1 = __builtin_amdgcn_alignbit(d2, d1, sh8),
-                               b2 = __builtin_amdgcn_alignbit(d3, d2, sh8);
-                uint64_t lo = ((uint64_t)b1 << 32) | b0;
-                if (len < 8) lo &= (1ull << (8 * len)) - 1;
-                uint64_t z = leb_pack8(lo);
-                if (len > 8) {          // groups 8, 9, 10 at shifts 56, 63, 70 & 63 = 6 (Rust release)
-                    const uint32_t hb = b2 & ((len >= 11) ? 0xFFFFFFu : (len == 10 ? 0xFFFFu : 0xFFu));
-                    z |= ((uint64_t)(hb & 0x7F) << 56) | ((uint64_t)((hb >> 8) & 0x7F) << 63) |
-                         ((uint64_t)((hb >> 16) & 0x7F) << 6);
-                }
-                dst[base + i] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
-            }
-            base += total;
-        }
-        __syncthreads();                                      // lb is restaged for the next region
+        base += total;
     }
 }
 
-// Irregular blobs: the reference loop, one lane per blob (only malformed streams get here); it
-// rewrites the blob's row (values past `cap` are counted, not stored) and its count.
+// Irregular blobs: the reference loop, one lane per blob (only malformed streams get here).
+// With out == nullptr it only counts.
 __global__ void varint_sequential_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ blob_off,
                                          uint32_t n_blobs, const uint32_t* __restrict__ blob_irregular,
                                          uint64_t* __restrict__ blob_count, int64_t* __restrict__ out,
@@ -353,10 +306,10 @@ __global__ void varint_sequential_kernel(const uint8_t* __restrict__ bytes, cons
             shift += 7;
             if (!(by & 0x80) || shift > 70) break;
         }
-        if (c < cap) out[(uint64_t)b * out_stride + c] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
+        if (out && c < cap) out[(uint64_t)b * out_stride + c] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
         ++c;
     }
-    blob_count[b] = c;
+    if (!out) blob_count[b] = c;
 }
 
 // ---------------- encode ----------------
@@ -369,6 +322,29 @@ __device__ __forceinline__ uint32_t varint_size(int64_t v) {
 constexpr uint32_t kEncChunk = 2048;          // elements per encode block
 constexpr uint32_t kEncPer = kEncChunk / kThreads;
 
+// sizes of each [row][chunk] block of elements
+__global__ __launch_bounds__(kThreads) void varint_size_kernel(const int64_t* __restrict__ vals, uint64_t len,
+                                                               uint64_t stride, uint32_t chunks,
+                                                               uint64_t* __restrict__ chunk_bytes) {
+    const uint32_t c = blockIdx.x, row = blockIdx.y;
+    const uint64_t e0 = (uint64_t)c * kEncChunk;
+    uint64_t n = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kEncPer; ++q) {
+        const uint64_t e = e0 + q * kThreads + threadIdx.x;
+        if (e < len) n += varint_size(vals[row * stride + e]);
+    }
+    __shared__ uint64_t red[kThreads / 64];
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t s = 0;
+        for (int i = 0; i < kThreads / 64; ++i) s += red[i];
+        chunk_bytes[(uint64_t)row * chunks + c] = s;
+    }
+}
+
 // inverse of leb_pack8: 7-bit groups of z -> bytes (group i in byte i), continuation bits not set
 __device__ __forceinline__ uint64_t leb_spread8(uint64_t z) {
     uint64_t x = z & 0x00FFFFFFFFFFFFFFull;
@@ -378,122 +354,97 @@ __device__ __forceinline__ uint64_t leb_spread8(uint64_t z) {
     return x;
 }
 
-constexpr uint32_t kEncTileChunks = 8;        // chunks per encode workgroup (16384 values)
-
-// One pass: a workgroup takes the next tile of up to 8 chunks of 2048 values (atomic ticket; tiles
-// numbered row by row, and the rows' payloads lie back to back), sizes the tile's varints (first
-// read of the values), gets the tile's byte offset from the look-back over all earlier tiles, then
-// per chunk reloads the values (from the caches), assembles the bytes in LDS at the chunk's offset
-// mod 4 (so LDS dwords line up with global dwords) and writes dwords for the interior, bytes for
-// the two partial ends (shared with the neighbouring chunks).  Bytes at or past dst_cap are not
-// written; row_end[row] = end offset of the row (its last tile writes it).
-__global__ __launch_bounds__(kThreads) void varint_encode_kernel(const int64_t* __restrict__ vals, uint64_t len,
-                                                                 uint64_t stride, uint64_t tiles_per_row,
-                                                                 unsigned long long* __restrict__ status,
-                                                                 unsigned int* __restrict__ ticket,
-                                                                 uint64_t* __restrict__ row_end,
-                                                                 unsigned int* __restrict__ err,
-                                                                 uint8_t* __restrict__ dst, uint64_t dst_cap) {
+// write: coalesced loads (element q * 256 + t of the chunk), one block-wide scan of the sizes per
+// q, bytes assembled in LDS at the chunk's global byte offset mod 4 (so LDS dwords line up with
+// global dwords), then dword stores for the interior and byte stores for the two partial ends
+// (shared with the neighbouring chunks).  chunk_off = row offset + exclusive scan of chunk_bytes.
+__global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* __restrict__ vals, uint64_t len,
+                                                                uint64_t stride, uint32_t chunks,
+                                                                const uint64_t* __restrict__ chunk_off,
+                                                                uint8_t* __restrict__ dst) {
+    const uint32_t c = blockIdx.x, row = blockIdx.y;
+    const uint64_t e0 = (uint64_t)c * kEncChunk;
     __shared__ uint32_t buf[(kEncChunk * 10 + 8) / 4];
     __shared__ uint32_t wsum[kThreads / 64];
-    __shared__ uint32_t cbytes[kEncTileChunks];
-    __shared__ uint64_t sh[2];
-    if (threadIdx.x == 0) sh[0] = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint64_t t = sh[0];
-    const uint64_t row = t / tiles_per_row, x = t - row * tiles_per_row;
-    const int64_t* rv = vals + row * stride;
-    const uint64_t c0 = x * kEncTileChunks, n_chunks = (len + kEncChunk - 1) / kEncChunk;
-    const uint32_t nc = (uint32_t)(n_chunks - c0 < kEncTileChunks ? n_chunks - c0 : kEncTileChunks);
-    // ---- phase 1: bytes per chunk ----
-    for (uint32_t k = 0; k < nc; ++k) {
-        const uint64_t e0 = (c0 + k) * kEncChunk;
-        uint32_t mine = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < kEncPer; ++q) {
-            const uint64_t e = e0 + q * kThreads + threadIdx.x;
-            mine += e < len ? varint_size(rv[e]) : 0u;
-        }
-        const uint32_t cb = block_sum(mine, wsum);
-        if (threadIdx.x == 0) cbytes[k] = cb;
-    }
-    __syncthreads();
-    uint32_t agg = 0;
-    for (uint32_t k = 0; k < nc; ++k) agg += cbytes[k];
-    if (threadIdx.x < 64) {                                   // wave 0: publish, look back, publish
-        uint64_t excl = 0;
-        if (t == 0) {
-            if (threadIdx.x == 0) lb_publish(status, kIncReady | agg);
-        } else {
-            if (threadIdx.x == 0) lb_publish(status + t, kAggReady | agg);
-            excl = lb_exclusive(status, t, 0, err);
-            if (threadIdx.x == 0) lb_publish(status + t, kIncReady | (excl + agg));
-        }
-        if (threadIdx.x == 0) {
-            if (x + 1 == tiles_per_row) row_end[row] = excl + agg;
-            sh[1] = excl;
-        }
-    }
-    __syncthreads();
-    // ---- phase 2: write chunk by chunk ----
-    uint64_t go = sh[1];
+    const uint64_t go = chunk_off[(uint64_t)row * chunks + c];
+    const uint32_t lead = (uint32_t)(go & 3);
     uint8_t* b8 = reinterpret_cast<uint8_t*>(buf);
-    for (uint32_t k = 0; k < nc; ++k) {
-        const uint64_t e0 = (c0 + k) * kEncChunk;
-        int64_t v[kEncPer];
-        uint32_t n[kEncPer];
+    int64_t v[kEncPer];
 #pragma unroll
-        for (uint32_t q = 0; q < kEncPer; ++q) {
-            const uint64_t e = e0 + q * kThreads + threadIdx.x;
-            v[q] = e < len ? rv[e] : 0;
-            n[q] = e < len ? varint_size(v[q]) : 0u;
-        }
-        const uint32_t lead = (uint32_t)(go & 3);
-        uint32_t base = lead;
-#pragma unroll
-        for (uint32_t q = 0; q < kEncPer; ++q) {
-            const uint64_t z = ((uint64_t)v[q] << 1) ^ (uint64_t)(v[q] >> 63);
-            uint32_t incl = n[q];
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t tt = __shfl_up(incl, o);
-                if ((threadIdx.x & 63) >= (uint32_t)o) incl += tt;
-            }
-            __syncthreads();                                 // wsum of the previous q consumed
-            if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
-            __syncthreads();
-            uint32_t off = base + incl - n[q], total = 0;
-            for (uint32_t w = 0; w < kThreads / 64; ++w) {
-                if (w < (threadIdx.x >> 6)) off += wsum[w];
-                total += wsum[w];
-            }
-            base += total;
-            // bytes: groups 0..7 from the spread, continuation bit on every byte but the last
-            const uint64_t lo = leb_spread8(z);
-            const uint32_t g8 = (uint32_t)(z >> 56) & 0x7Fu, g9 = (uint32_t)(z >> 63);
-#pragma unroll
-            for (uint32_t i = 0; i < 8; ++i)
-                if (i < n[q]) b8[off + i] = (uint8_t)(i + 1 < n[q] ? (lo >> (8 * i)) | 0x80 : (lo >> (8 * i)) & 0x7F);
-            if (n[q] > 8) b8[off + 8] = (uint8_t)(g8 | (n[q] > 9 ? 0x80u : 0u));
-            if (n[q] > 9) b8[off + 9] = (uint8_t)g9;
-        }
-        __syncthreads();
-        const uint32_t endb = base;                          // lead + chunk bytes
-        const uint64_t g0 = go & ~3ull;
-        uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + g0);
-        uint8_t* d8 = dst + g0;
-        const uint32_t nw = (endb + 3) / 4;
-        for (uint32_t kk = threadIdx.x; kk < nw; kk += kThreads) {
-            const uint32_t lo = kk * 4, hi = lo + 4;
-            if (lo >= lead && hi <= endb && g0 + hi <= dst_cap) {
-                d32[kk] = buf[kk];
-            } else {
-                for (uint32_t i = lo; i < hi; ++i)
-                    if (i >= lead && i < endb && g0 + i < dst_cap) d8[i] = b8[i];
-            }
-        }
-        go += endb - lead;
-        __syncthreads();                                     // buf is reassembled for the next chunk
+    for (uint32_t q = 0; q < kEncPer; ++q) {
+        const uint64_t e = e0 + q * kThreads + threadIdx.x;
+        v[q] = e < len ? vals[row * stride + e] : 0;
     }
+    uint32_t base = lead;
+#pragma unroll
+    for (uint32_t q = 0; q < kEncPer; ++q) {
+        const bool in = e0 + q * kThreads + threadIdx.x < len;
+        const uint64_t z = ((uint64_t)v[q] << 1) ^ (uint64_t)(v[q] >> 63);
+        const uint32_t n = in ? varint_size(v[q]) : 0u;
+        uint32_t incl = n;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o);
+            if ((threadIdx.x & 63) >= (uint32_t)o) incl += t;
+        }
+        __syncthreads();                                     // wsum of the previous q consumed
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        uint32_t off = base + incl - n, total = 0;
+        for (uint32_t w = 0; w < kThreads / 64; ++w) {
+            if (w < (threadIdx.x >> 6)) off += wsum[w];
+            total += wsum[w];
+        }
+        base += total;
+        // bytes: groups 0..7 from the spread, continuation bit on every byte but the last
+        const uint64_t lo = leb_spread8(z);
+        const uint32_t g8 = (uint32_t)(z >> 56) & 0x7Fu, g9 = (uint32_t)(z >> 63);
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i)
+            if (i < n) b8[off + i] = (uint8_t)(i + 1 < n ? (lo >> (8 * i)) | 0x80 : (lo >> (8 * i)) & 0x7F);
+        if (n > 8) b8[off + 8] = (uint8_t)(g8 | (n > 9 ? 0x80u : 0u));
+        if (n > 9) b8[off + 9] = (uint8_t)g9;
+    }
+    __syncthreads();
+    const uint32_t end = base;                               // lead + chunk bytes
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + (go & ~3ull));
+    uint8_t* d8 = dst + (go & ~3ull);
+    const uint32_t nw = (end + 3) / 4;
+    for (uint32_t k = threadIdx.x; k < nw; k += kThreads) {
+        const uint32_t lo = k * 4, hi = lo + 4;
+        if (lo >= lead && hi <= end) {
+            d32[k] = buf[k];
+        } else {
+            for (uint32_t i = lo; i < hi; ++i)
+                if (i >= lead && i < end) d8[i] = b8[i];
+        }
+    }
+}
+
+// exclusive scan of chunk_bytes per row (one block per row) + row base; row_bytes = total
+__global__ __launch_bounds__(kThreads) void varint_offsets_kernel(const uint64_t* __restrict__ chunk_bytes,
+                                                                  uint32_t chunks, const uint64_t* __restrict__ row_base,
+                                                                  uint64_t* __restrict__ chunk_off,
+                                                                  uint64_t* __restrict__ row_bytes) {
+    const uint32_t row = blockIdx.x;
+    __shared__ uint64_t part[kThreads];
+    uint64_t carry = row_base ? row_base[row] : 0, total = 0;
+    for (uint32_t base = 0; base < chunks; base += kThreads) {
+        const uint32_t c = base + threadIdx.x;
+        const uint64_t v = c < chunks ? chunk_bytes[(uint64_t)row * chunks + c] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < kThreads; o <<= 1) {
+            const uint64_t add = threadIdx.x >= (uint32_t)o ? part[threadIdx.x - o] : 0;
+            __syncthreads();
+            part[threadIdx.x] += add;
+            __syncthreads();
+        }
+        if (c < chunks) chunk_off[(uint64_t)row * chunks + c] = carry + part[threadIdx.x] - v;
+        carry += part[kThreads - 1];
+        total += part[kThreads - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && row_bytes) row_bytes[row] = total;
 }
 
 }  // namespace
@@ -501,115 +452,128 @@ __global__ __launch_bounds__(kThreads) void varint_encode_kernel(const int64_t* 
 // ---------------- host-side planning ----------------
 void varint_plan(const uint64_t* blob_off, uint64_t n_blobs, VarintPlan* plan) {
     plan->blob_region.assign(n_blobs + 1, 0);
-    plan->blob_tile.assign(n_blobs + 1, 0);
     plan->max_regions = 0;
-    uint64_t R = 0, T = 0;
+    uint64_t R = 0;
     for (uint64_t b = 0; b < n_blobs; ++b) {
         plan->blob_region[b] = R;
-        plan->blob_tile[b] = T;
         const uint64_t s = blob_off[b], e = blob_off[b + 1];
         const uint64_t nr = e > s ? (e - 1) / kRegionBytes - s / kRegionBytes + 1 : 0;
         R += nr;
-        T += (nr + kTileRegions - 1) / kTileRegions;
         if (nr > plan->max_regions) plan->max_regions = nr;
     }
     plan->blob_region[n_blobs] = R;
-    plan->blob_tile[n_blobs] = T;
     plan->regions = R;
-    plan->tiles = T;
 }
 
-// Layout of the device workspace of the decode.
+// Layout of the device workspace for the decode passes.
 struct DecodeWork {
-    unsigned long long* status; unsigned int* ticket; unsigned int* err;
-    uint64_t* blob_off; uint64_t* blob_tile; uint32_t* irregular; uint64_t* blob_count;
+    uint32_t* region_count; uint64_t* region_base;
+    uint64_t* blob_off; uint64_t* blob_region; uint32_t* irregular; uint64_t* blob_count;
 };
 static DecodeWork carve(void* work, size_t R, uint64_t n_blobs) {
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     char* p = static_cast<char*>(work);
     DecodeWork w;
-    w.status = (unsigned long long*)p; p += up(R * 8);
-    w.ticket = (unsigned int*)p; w.err = w.ticket + 1; p += 256;
+    w.region_base = (uint64_t*)p; p += up(R * 8);
+    w.region_count = (uint32_t*)p; p += up(R * 4);
     w.blob_off = (uint64_t*)p; p += up((n_blobs + 1) * 8);
-    w.blob_tile = (uint64_t*)p; p += up((n_blobs + 1) * 8);
+    w.blob_region = (uint64_t*)p; p += up((n_blobs + 1) * 8);
     w.irregular = (uint32_t*)p; p += up(n_blobs * 4);
     w.blob_count = (uint64_t*)p;
     return w;
 }
 size_t varint_decode_work_bytes(size_t regions, uint64_t n_blobs) {
-    return regions * 8 + (n_blobs + 1) * 16 + n_blobs * 12 + 8 * 256;
+    return regions * 12 + (n_blobs + 1) * 16 + n_blobs * 12 + 8 * 256;
 }
 
-hipError_t launch_varint_decode(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
-                                const VarintPlan& plan, void* work, int64_t* out, uint64_t out_stride,
-                                uint64_t* counts_host, hipStream_t s) {
-    const size_t T = plan.tiles;
-    DecodeWork w = carve(work, T, n_blobs);
+hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
+                               const VarintPlan& plan, void* work, uint64_t* counts_host, bool* irregular_any,
+                               hipStream_t s) {
+    const size_t R = plan.regions;
+    DecodeWork w = carve(work, R, n_blobs);
     hipError_t e;
-    if (n_blobs == 0) return hipSuccess;
     if ((e = hipMemcpyAsync(w.blob_off, blob_off_host, (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(w.blob_tile, plan.blob_tile.data(), (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(w.status, 0, ((T * 8 + 255) & ~(size_t)255) + 256, s)) != hipSuccess) return e;   // + ticket, err
+    if ((e = hipMemcpyAsync(w.blob_region, plan.blob_region.data(), (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.irregular, 0, n_blobs * 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(w.blob_count, 0, n_blobs * 8, s)) != hipSuccess) return e;      // empty blobs: 0
-    if (T) {
-        hipLaunchKernelGGL(varint_decode_kernel, dim3((unsigned)T), dim3(kThreads), 0, s, bytes, w.blob_tile,
-                           w.blob_off, n_blobs, w.status, w.ticket, w.irregular, w.blob_count, w.err, out, out_stride);
+    for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
+        const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
+        hipLaunchKernelGGL(varint_count_kernel, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s, bytes,
+                           w.blob_region, w.blob_off, (uint32_t)y0, w.region_count, w.irregular);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    hipLaunchKernelGGL(varint_scan_kernel, dim3((unsigned)n_blobs), dim3(kThreads), 0, s, w.region_count,
+                       w.blob_region, w.region_base, w.blob_count);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(varint_sequential_kernel, dim3((unsigned)((n_blobs + 63) / 64)), dim3(64), 0, s, bytes,
+                       w.blob_off, (uint32_t)n_blobs, w.irregular, w.blob_count, (int64_t*)nullptr, 0, 0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     std::vector<uint32_t> irr(n_blobs);
-    uint32_t errf = 0;
+    if ((e = hipMemcpyAsync(counts_host, w.blob_count, n_blobs * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipMemcpyAsync(irr.data(), w.irregular, n_blobs * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(&errf, w.err, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    if (errf) return hipErrorUnknown;              // a look-back spin ran out (never expected)
-    bool irregular_any = false;
-    for (uint64_t b = 0; b < n_blobs; ++b) irregular_any |= irr[b] != 0;
-    if (irregular_any) {                           // malformed blobs: the reference loop, row and count
-        hipLaunchKernelGGL(varint_sequential_kernel, dim3((unsigned)((n_blobs + 63) / 64)), dim3(64), 0, s, bytes,
-                           w.blob_off, (uint32_t)n_blobs, w.irregular, w.blob_count, out, out_stride, out_stride);
+    *irregular_any = false;
+    for (uint64_t b = 0; b < n_blobs; ++b) *irregular_any |= irr[b] != 0;
+    return hipSuccess;
+}
+
+hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
+                                int64_t* out, uint64_t out_stride, uint64_t len, bool irregular_any,
+                                hipStream_t s) {
+    const size_t R = plan.regions;
+    DecodeWork w = carve(work, R, n_blobs);
+    hipError_t e;
+    for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
+        const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
+        hipLaunchKernelGGL(varint_decode_kernel, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s, bytes,
+                           w.blob_region, w.blob_off, (uint32_t)y0, w.region_base, w.irregular, out, out_stride);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if ((e = hipMemcpyAsync(counts_host, w.blob_count, n_blobs * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    return hipStreamSynchronize(s);
+    if (irregular_any) {
+        hipLaunchKernelGGL(varint_sequential_kernel, dim3((unsigned)((n_blobs + 63) / 64)), dim3(64), 0, s, bytes,
+                           w.blob_off, (uint32_t)n_blobs, w.irregular, w.blob_count, out, out_stride, len);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 size_t varint_encode_work_bytes(uint64_t rows, uint64_t len) {
     const uint64_t chunks = (len + kEncChunk - 1) / kEncChunk;
-    const uint64_t tiles = (chunks + kEncTileChunks - 1) / kEncTileChunks;
-    return rows * (tiles ? tiles : 1) * 8 + rows * 8 + 1024;
+    return 2 * rows * (chunks ? chunks : 1) * 8 + 2 * rows * 8 + 1024;
 }
 
 hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len, uint64_t stride, uint8_t* dst,
                                 uint64_t dst_cap, void* work, uint64_t* row_bytes_host, hipStream_t s) {
     const uint64_t chunks = (len + kEncChunk - 1) / kEncChunk;
-    const uint64_t tiles = (chunks + kEncTileChunks - 1) / kEncTileChunks;
     if (rows == 0) return hipSuccess;
-    if (tiles == 0) {
+    uint64_t* chunk_bytes = static_cast<uint64_t*>(work);
+    uint64_t* chunk_off = chunk_bytes + rows * (chunks ? chunks : 1);
+    uint64_t* row_base = chunk_off + rows * (chunks ? chunks : 1);
+    uint64_t* rbytes = row_base + rows;
+    hipError_t e;
+    if (chunks == 0) {
         for (uint64_t r = 0; r < rows; ++r) row_bytes_host[r] = 0;
         return hipSuccess;
     }
-    if (rows * tiles >= ((uint64_t)1 << 32)) return hipErrorInvalidValue;
-    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    char* p = static_cast<char*>(work);
-    unsigned long long* status = reinterpret_cast<unsigned long long*>(p);
-    unsigned int* ticket = reinterpret_cast<unsigned int*>(p + up(rows * tiles * 8));
-    unsigned int* err = ticket + 1;
-    uint64_t* row_end = reinterpret_cast<uint64_t*>(p + up(rows * tiles * 8) + 256);
-    hipError_t e;
-    if ((e = hipMemsetAsync(status, 0, up(rows * tiles * 8) + 256, s)) != hipSuccess) return e;   // + ticket, err
-    hipLaunchKernelGGL(varint_encode_kernel, dim3((unsigned)(rows * tiles)), dim3(kThreads), 0, s, vals, len, stride,
-                       tiles, status, ticket, row_end, err, dst, dst_cap);
+    hipLaunchKernelGGL(varint_size_kernel, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s, vals, len,
+                       stride, (uint32_t)chunks, chunk_bytes);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    std::vector<uint64_t> ends(rows);
-    uint32_t errf = 0;
-    if ((e = hipMemcpyAsync(ends.data(), row_end, rows * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(&errf, err, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    // per-row totals first (row_base = nullptr), then the host places rows back to back
+    hipLaunchKernelGGL(varint_offsets_kernel, dim3((unsigned)rows), dim3(kThreads), 0, s, chunk_bytes,
+                       (uint32_t)chunks, (const uint64_t*)nullptr, chunk_off, rbytes);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(row_bytes_host, rbytes, rows * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    if (errf) return hipErrorUnknown;
-    for (uint64_t r = 0; r < rows; ++r) row_bytes_host[r] = ends[r] - (r ? ends[r - 1] : 0);
-    if (ends[rows - 1] > dst_cap) return hipErrorInvalidValue;    // nothing past dst_cap was written
-    return hipSuccess;
+    std::vector<uint64_t> base(rows);
+    uint64_t acc = 0;
+    for (uint64_t r = 0; r < rows; ++r) { base[r] = acc; acc += row_bytes_host[r]; }
+    if (acc > dst_cap) return hipErrorInvalidValue;
+    if ((e = hipMemcpyAsync(row_base, base.data(), rows * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(varint_offsets_kernel, dim3((unsigned)rows), dim3(kThreads), 0, s, chunk_bytes,
+                       (uint32_t)chunks, (const uint64_t*)row_base, chunk_off, (uint64_t*)nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(varint_write_kernel, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s, vals, len,
+                       stride, (uint32_t)chunks, chunk_off, dst);
+    return hipGetLastError();
 }
 
 }  // namespace sda

@@ -697,38 +697,29 @@ sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64
 // ---------------- share payload codec (sodium.rs:36-41 / :82-88) ----------------
 namespace {
 
-// Decode N device-resident blobs into out [N][out_stride] in one pass; counts[n] (host) = values
-// per blob (values past out_stride are counted, not stored).
-sda_status codec_decode(sda_engine* h, const uint8_t* bytes, const uint64_t* blob_off, uint64_t n_blobs,
-                        int64_t* out, uint64_t out_stride, uint64_t* counts, hipStream_t st) {
+// Plan + count N device-resident blobs; counts[n] on the host.
+sda_status codec_count(sda_engine* h, const uint8_t* bytes, const uint64_t* blob_off, uint64_t n_blobs,
+                       sda::VarintPlan* plan, uint64_t* counts, bool* irregular, hipStream_t st) {
     if (((uintptr_t)bytes & 15) != 0) return fail(SDA_ERR_INVALID_ARGUMENT, "byte buffer must be 16-byte aligned");
     for (uint64_t b = 0; b < n_blobs; ++b)
         if (blob_off[b + 1] < blob_off[b]) return fail(SDA_ERR_INVALID_ARGUMENT, "blob offsets must be non-decreasing");
-    sda::VarintPlan plan;
-    sda::varint_plan(blob_off, n_blobs, &plan);
-    if (plan.regions >= ((uint64_t)1 << 32)) return fail(SDA_ERR_UNSUPPORTED, "more than 2^32 decode regions");
+    sda::varint_plan(blob_off, n_blobs, plan);
     if (sda_status e = ensure(&h->codec_work, &h->codec_work_bytes,
-                              sda::varint_decode_work_bytes(plan.tiles, n_blobs)))
+                              sda::varint_decode_work_bytes(plan->regions, n_blobs)))
         return e;
-    HIP_TRY(sda::launch_varint_decode(bytes, blob_off, n_blobs, plan, h->codec_work, out, out_stride, counts, st));
+    HIP_TRY(sda::launch_varint_count(bytes, blob_off, n_blobs, *plan, h->codec_work, counts, irregular, st));
     return SDA_OK;
 }
 
-// decode + combiner.rs:16-28 over device-resident blobs; out (device) gets out_len = count of blob 0.
-// The decoded matrix is [N][stride] with stride = min(out_cap, longest blob) (a value takes >= 1 byte).
+// decode + combiner.rs:16-28 over device-resident blobs; out (device) gets out_len = count of blob 0
 sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const uint64_t* blob_off, uint64_t n_blobs,
                           int64_t* out, uint64_t out_cap, uint64_t* out_len, hipStream_t st) {
     *out_len = 0;
     if (n_blobs == 0) return ok();                                  // combiner.rs:17: empty input
-    uint64_t longest = 0;
-    for (uint64_t b = 0; b < n_blobs; ++b)
-        if (blob_off[b + 1] > blob_off[b] && blob_off[b + 1] - blob_off[b] > longest) longest = blob_off[b + 1] - blob_off[b];
-    uint64_t stride = out_cap < longest ? out_cap : longest;
-    if (stride == 0) stride = 1;
-    if (sda_status e = ensure(&h->codec_mat, &h->codec_mat_bytes, n_blobs * stride * 8)) return e;
-    int64_t* mat = static_cast<int64_t*>(h->codec_mat);
+    sda::VarintPlan plan;
     std::vector<uint64_t> counts(n_blobs);
-    if (sda_status e = codec_decode(h, bytes, blob_off, n_blobs, mat, stride, counts.data(), st)) return e;
+    bool irregular = false;
+    if (sda_status e = codec_count(h, bytes, blob_off, n_blobs, &plan, counts.data(), &irregular, st)) return e;
     const uint64_t dim = counts[0];
     for (uint64_t i = 1; i < n_blobs; ++i)
         if (counts[i] != dim)
@@ -741,7 +732,10 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
     if (out_cap < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
     *out_len = dim;
     if (dim == 0) return ok();
-    HIP_TRY(sda::launch_combine_exact(mat, n_blobs, dim, stride, out, mm, st));
+    if (sda_status e = ensure(&h->codec_mat, &h->codec_mat_bytes, n_blobs * dim * 8)) return e;
+    int64_t* mat = static_cast<int64_t*>(h->codec_mat);
+    HIP_TRY(sda::launch_varint_decode(bytes, n_blobs, plan, h->codec_work, mat, dim, dim, irregular, st));
+    HIP_TRY(sda::launch_combine_exact(mat, n_blobs, dim, dim, out, mm, st));
     return SDA_OK;
 }
 
@@ -800,10 +794,13 @@ sda_status sda_varint_decode(sda_engine* h, const uint8_t* bytes, uint64_t n_byt
     const uint8_t* const blobs[1] = {bytes};
     if (sda_status st = upload_blobs(h, blobs, &n_bytes, 1, &a, &db, &off)) return st;
     int64_t* dv = a.take<int64_t>(n_bytes + 1);
-    uint64_t count = 0;                                             // <= n_bytes: a value takes >= 1 byte
-    if (sda_status st = codec_decode(h, db, off.data(), 1, dv, n_bytes + 1, &count, h->stream)) return st;
+    sda::VarintPlan plan;
+    uint64_t count = 0;
+    bool irregular = false;
+    if (sda_status st = codec_count(h, db, off.data(), 1, &plan, &count, &irregular, h->stream)) return st;
     if (count > out_cap) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small (%llu values)",
                                      (unsigned long long)count);
+    HIP_TRY(sda::launch_varint_decode(db, 1, plan, h->codec_work, dv, count, count, irregular, h->stream));
     if (count) HIP_TRY(hipMemcpyAsync(out, dv, count * 8, hipMemcpyDeviceToHost, h->stream));
     *out_len = count;
     return finish(h);
@@ -824,9 +821,9 @@ sda_status sda_clerk_decode_combine(sda_engine* h, const sda_sharing_scheme* s, 
     if (sda_status st = upload_blobs(h, blobs, blob_lens, n_blobs, &a, &db, &off)) return st;
     int64_t* dout = a.take<int64_t>(total + 1);
     uint64_t len = 0;
-    if (sda_status st = decode_combine(h, s->modulus, db, off.data(), n_blobs, dout, out_cap < total + 1 ? out_cap : total + 1,
-                                       &len, h->stream))
+    if (sda_status st = decode_combine(h, s->modulus, db, off.data(), n_blobs, dout, (uint64_t)-1, &len, h->stream))
         return st;
+    if (out_cap < len) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
     if (len) HIP_TRY(hipMemcpyAsync(out, dout, len * 8, hipMemcpyDeviceToHost, h->stream));
     *out_len = len;
     return finish(h);
@@ -837,11 +834,14 @@ sda_status sda_varint_decode_dev(sda_engine* h, const uint8_t* bytes, const uint
     if (!h || !blob_off || !counts || (n_blobs && (!bytes || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = pick(h, stream);
-    if (sda_status e = codec_decode(h, bytes, blob_off, n_blobs, out, out_stride, counts, st)) return e;
+    sda::VarintPlan plan;
+    bool irregular = false;
+    if (sda_status e = codec_count(h, bytes, blob_off, n_blobs, &plan, counts, &irregular, st)) return e;
     for (uint64_t i = 0; i < n_blobs; ++i)
         if (counts[i] > out_stride)
-            return fail(SDA_ERR_INVALID_ARGUMENT, "blob %llu decodes to %llu values > out_stride (out holds the first %llu)",
-                        (unsigned long long)i, (unsigned long long)counts[i], (unsigned long long)out_stride);
+            return fail(SDA_ERR_INVALID_ARGUMENT, "blob %llu decodes to %llu values > out_stride",
+                        (unsigned long long)i, (unsigned long long)counts[i]);
+    HIP_TRY(sda::launch_varint_decode(bytes, n_blobs, plan, h->codec_work, out, out_stride, out_stride, irregular, st));
     return ok();
 }
 

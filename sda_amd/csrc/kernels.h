@@ -78,27 +78,26 @@ hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indic
                                 DeviceTable& tab, void* log_buf, hipStream_t s);
 
 // ---- codec.hip (share payload codec: sodium.rs:36-41 / :82-88, integer-encoding 1.0 VarInt) ----
-// Host-side plan of the decode: blobs are split into 16 KiB regions aligned to the (16-byte
+// Host-side plan of the decode: blobs are split into 4 KiB regions aligned to the (16-byte
 // aligned) byte buffer; a region shared by two blobs appears once per blob.
 struct VarintPlan {
     std::vector<uint64_t> blob_region;   // [n_blobs + 1] first region of each blob (prefix sum)
-    std::vector<uint64_t> blob_tile;     // [n_blobs + 1] first tile (group of 8 regions) of each blob
     uint64_t regions = 0;
-    uint64_t tiles = 0;
-    uint64_t max_regions = 0;            // regions of the largest blob
+    uint64_t max_regions = 0;            // regions of the largest blob (grid.x)
 };
 void varint_plan(const uint64_t* blob_off, uint64_t n_blobs, VarintPlan* plan);
-size_t varint_decode_work_bytes(size_t tiles, uint64_t n_blobs);
-// decode every blob into out + blob * out_stride in one pass over the payload (values at index >=
-// out_stride are counted, not stored); counts_host[n_blobs] = values per blob (synchronous).
-// hipErrorUnknown if the look-back failed (never expected).
-hipError_t launch_varint_decode(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
-                                const VarintPlan& plan, void* work, int64_t* out, uint64_t out_stride,
-                                uint64_t* counts_host, hipStream_t s);
+size_t varint_decode_work_bytes(size_t regions, uint64_t n_blobs);
+// element count of every blob (synchronous: copies n_blobs counts to the host)
+hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
+                               const VarintPlan& plan, void* work, uint64_t* counts_host, bool* irregular_any,
+                               hipStream_t s);
+// decode every blob into out + blob * out_stride (after launch_varint_count on the same work)
+hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
+                                int64_t* out, uint64_t out_stride, uint64_t len, bool irregular_any,
+                                hipStream_t s);
 size_t varint_encode_work_bytes(uint64_t rows, uint64_t len);
-// encode rows [rows][stride] (first len elements) back to back into dst in one pass; row_bytes_host
-// gets each row's byte count (synchronous).  hipErrorInvalidValue if dst_cap is too small (no byte
-// at or past dst_cap is written).
+// encode rows [rows][stride] (first len elements) back to back into dst; row_bytes_host gets each
+// row's byte count (synchronous).  hipErrorInvalidValue if dst_cap is too small.
 hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len, uint64_t stride, uint8_t* dst,
                                 uint64_t dst_cap, void* work, uint64_t* row_bytes_host, hipStream_t s);
 
