@@ -334,6 +334,15 @@ def main():
             "reveal_canonical_ms": c_ms, "reveal_canonical_GBps": rev_bytes / (c_ms * 1e-3) / 1e9,
             "reveal_clerks": len(idx),
         }
+        waves = V * ((B + 255) // 256) * 4              # 256-lane workgroups (L = 16 share-gen and reveal)
+        for key, ms in (("gen_exact", g_ms), ("gen_canonical", gc_ms), ("reveal_exact", x_ms),
+                        ("reveal_canonical", c_ms)):
+            r = valu_roofline(key, ms, waves)
+            if r:
+                side["shamir"][key + "_valu"] = r
+        ex = side["shamir"].get("gen_exact_valu")
+        if ex:      # integer-op throughput of share-gen (north star: "integer-op throughput in rocprof")
+            side["shamir"]["int_ops_per_s"] = ex["achieved"] * 1e12
         log(f"[shamir] {json.dumps(side['shamir'])}")
         del sec, drw, sh, sub, rev
     if not args.no_side and args.only in (None, "chacha"):
@@ -349,6 +358,9 @@ def main():
         side["chacha"] = {"config": f"ChaCha mask combine, {Ns} seeds x 1M-dim", "ms": c_ms,
                           "mask_elems_per_s": Ns * Dc / (c_ms * 1e-3),
                           "chacha_blocks_per_s": Ns * Dc / 8 / (c_ms * 1e-3)}
+        r = valu_roofline("chacha_combine", c_ms, None)
+        if r:
+            side["chacha"]["roofline"] = r
         log(f"[chacha] {json.dumps(side['chacha'])}")
 
     if not args.no_side and args.only in (None, "codec"):
@@ -529,6 +541,28 @@ def main():
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def valu_roofline(key, ms, waves):
+    """VALU issue roofline of an integer kernel (scripts/valu_mix.py -> profiles/valu_roofline.json):
+    lane-ops per launch = SQ_INSTS_VALU (PMC, at this configuration) x 64, or the static VALU count of
+    the straight-line kernel x its waves; achieved = lane-ops / live kernel time; peak = the kernel's
+    instruction mix priced at the measured tools/ubench_int issue rates."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "valu_roofline.json")) as f:
+            k = json.load(f)["kernels"][key]
+    except (OSError, ValueError, KeyError):
+        return None
+    if k.get("pmc_valu_insts_per_launch") and (waves is None or k.get("pmc_waves") == waves):
+        insts, src = k["pmc_valu_insts_per_launch"], "PMC SQ_INSTS_VALU"
+    elif waves is not None:
+        insts, src = k["static_valu"] * waves, "static VALU count x waves"
+    else:
+        return None
+    achieved = insts * 64 / (ms * 1e-3) / 1e12
+    return {"bound": "valu", "achieved": round(achieved, 3), "peak": k["mix_ceiling_T_lane_ops"],
+            "unit": "T lane-ops/s", "frac": round(achieved / k["mix_ceiling_T_lane_ops"], 4),
+            "valu_insts_per_launch": insts, "source": src}
 
 
 def traffic_from_profile(N, D):

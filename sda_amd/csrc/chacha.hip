@@ -15,6 +15,8 @@
 // of that stream by one word pair: the main kernel adds the un-shifted draw and records the
 // (seed, pair) event; a host-driven fix-up then recomputes only the affected stream suffixes
 // (probability < 2^-33 per draw for 31-bit m).  Roofline: VALU (~1000 int32 ops per block).
+#include <stdlib.h>
+
 #include <algorithm>
 #include <vector>
 
@@ -409,9 +411,9 @@ static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_
     const uint64_t gx = (n_blk + 255) / 256;
     const uint64_t mm = (uint64_t)modulus;
     const bool lazy = mm <= (1ull << 32);
-    // Seeds split over grid.y chunks so that the grid fills the chip in whole rounds of resident
-    // workgroups: minimise rounds(C) x seeds-per-chunk(C).  The u64 accumulators receive one
-    // canonical partial (< m) per chunk (headroom).
+    // Seeds split over grid.y chunks until the grid holds one full round of resident workgroups (the
+    // kernel is VALU-bound: more chunks only add atomic merges -- A/B in profiles/r02/ab_chacha.txt).
+    // The u64 accumulators receive one canonical partial (< m) per chunk (headroom).
     static int cap_wgs = 0;
     if (cap_wgs == 0) {
         int dev = 0, cus = 0, per_cu = 0;
@@ -429,13 +431,13 @@ static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_
         cap_wgs = (cus > 0 && per_cu > 0) ? cus * per_cu : 2048;
     }
     uint64_t max_c = n_seeds ? n_seeds : 1;
-    if (max_c > 4096) max_c = 4096;
+    if (max_c > 65535) max_c = 65535;
     if (M.m > 1 && max_c > UINT64_MAX / (M.m - 1)) max_c = UINT64_MAX / (M.m - 1);
-    uint64_t chunks = 1, best = UINT64_MAX;
-    for (uint64_t c = 1; c <= max_c; ++c) {
-        const uint64_t per_c = (n_seeds + c - 1) / c;
-        const uint64_t cost = ((gx * c + cap_wgs - 1) / cap_wgs) * (per_c ? per_c : 1);
-        if (cost < best) { best = cost; chunks = c; }
+    uint64_t chunks = ((uint64_t)cap_wgs + gx - 1) / gx;
+    if (chunks > max_c) chunks = max_c;
+    if (const char* ce = getenv("SDA_CHACHA_CHUNKS")) {          // A/B knob
+        const uint64_t c = strtoull(ce, nullptr, 10);
+        if (c >= 1 && c <= max_c) chunks = c;
     }
     const uint64_t per = n_seeds ? (n_seeds + chunks - 1) / chunks : 0;
     const bool direct = chunks == 1;             // results stored straight into `out`
@@ -446,18 +448,14 @@ static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_
     {
         const dim3 grid((unsigned)gx, (unsigned)chunks);
         const uint64_t r64 = lazy ? (UINT64_MAX % mm + 1) % mm : 0;          // 2^64 mod m
-        if (lazy && direct)
-            hipLaunchKernelGGL((chacha_combine_kernel<true, true>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per, D,
-                               dst, M, zone, r64, log);
-        else if (lazy)
-            hipLaunchKernelGGL((chacha_combine_kernel<true, false>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per,
-                               D, dst, M, zone, r64, log);
-        else if (direct)
-            hipLaunchKernelGGL((chacha_combine_kernel<false, true>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per,
-                               D, dst, M, zone, r64, log);
-        else
-            hipLaunchKernelGGL((chacha_combine_kernel<false, false>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per,
-                               D, dst, M, zone, r64, log);
+#define SDA_CHACHA_LAUNCH(L, DI)                                                                          \
+    hipLaunchKernelGGL((chacha_combine_kernel<L, DI>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per, D, \
+                       dst, M, zone, r64, log)
+        if (lazy && direct) SDA_CHACHA_LAUNCH(true, true);
+        else if (lazy) SDA_CHACHA_LAUNCH(true, false);
+        else if (direct) SDA_CHACHA_LAUNCH(false, true);
+        else SDA_CHACHA_LAUNCH(false, false);
+#undef SDA_CHACHA_LAUNCH
         if ((e = hipGetLastError()) != hipSuccess) return e;
         // read the rejection log (a few bytes) -- the call is synchronous anyway
         unsigned long long n_rej = 0;
