@@ -50,18 +50,24 @@ __device__ __forceinline__ void reveal_flush(int64_t* lds_o, int64_t* o, uint64_
 // branch-free indices, so every load can be issued before the first wait; each share is turned into
 // its (sign, residue) pair as it lands, so no i64 copy stays live.  Returns whether every share lies
 // in (-p, p).
-template <int MMAX>
+template <int MMAX, bool EAGER>
 __device__ __forceinline__ bool load_points(const int64_t* __restrict__ sh, uint64_t B, uint32_t m, uint32_t p,
                                             FE (&s)[MMAX]) {
     const int64_t P = (int64_t)p;
     s[0] = FE{0, 0};
     bool in_range = true;
-    static_for<1, MMAX>([&](auto i) {
-        const int64_t v = sh[(uint64_t)((uint32_t)i < m ? i - 1 : 0) * B];
+    auto take = [&](auto i, int64_t v) {
         in_range = in_range && ((uint32_t)i >= m || (uint64_t)(v + (P - 1)) < (uint64_t)(2 * P - 1));
         const int32_t x = (uint32_t)i < m ? (int32_t)v : 0;
         s[i] = FE{x, canon32(x, p)};
-    });
+    };
+    if constexpr (EAGER) {               // every load first (all in flight), then convert
+        int64_t v[MMAX];
+        static_for<1, MMAX>([&](auto i) { v[i] = sh[(uint64_t)((uint32_t)i < m ? i - 1 : 0) * B]; });
+        static_for<1, MMAX>([&](auto i) { take(i, v[i]); });
+    } else {                             // convert as they land (no i64 copies live: fewer VGPRs)
+        static_for<1, MMAX>([&](auto i) { take(i, sh[(uint64_t)((uint32_t)i < m ? i - 1 : 0) * B]); });
+    }
     return in_range;
 }
 
@@ -163,7 +169,7 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
     const uint32_t lim = STAGED ? k : (b * k < D ? (uint32_t)(D - b * k < k ? D - b * k : k) : 0u);
 
     FE s[MMAX];
-    const bool in_range = load_points<MMAX>(sh, B, m, M.p, s);
+    const bool in_range = load_points<MMAX, (KU > 0)>(sh, B, m, M.p, s);
     const bool redo = !in_range || newton_reveal<MMAX, KU, LAZY, FULL>(s, m, k, tab, M, dst, lim);
     if (redo && live) {                                  // -> packed_reveal_fixup_kernel
         const uint32_t slot = atomicAdd(log, 1u);
@@ -219,7 +225,7 @@ __global__ __launch_bounds__(64) void packed_reveal_fixup_kernel(const int64_t* 
         const int64_t* sh = shares + vec * (uint64_t)n_idx * B + b;
         int64_t* dst = out + vec * D + b * k;
         FE s[MMAX];
-        if (load_points<MMAX>(sh, B, m, M.p, s)) newton_reveal<MMAX, KU, false, false>(s, m, k, tab, M, dst, lim);
+        if (load_points<MMAX, false>(sh, B, m, M.p, s)) newton_reveal<MMAX, KU, false, false>(s, m, k, tab, M, dst, lim);
         else reveal_exact_generic(sh, B, m, k, tab, M.p, dst, lim);
     }
 }
@@ -243,11 +249,17 @@ __global__ __launch_bounds__(256) void packed_reveal_canon_kernel(const int64_t*
 
     uint32_t S[NMAX];
     bool in_range = true;
-    static_for<0, NMAX>([&](auto i) {
-        const int64_t v = sh[(uint64_t)((uint32_t)i < n_idx ? i : 0) * B];
+    auto take = [&](auto i, int64_t v) {
         in_range = in_range && ((uint32_t)i >= n_idx || (uint64_t)(v + (P - 1)) < (uint64_t)(2 * P - 1));
         S[i] = (uint32_t)i < n_idx ? canon32((int32_t)v, p) : 0u;
-    });
+    };
+    if constexpr (NMAX <= 64) {          // every load first (all in flight), then convert
+        int64_t v[NMAX];
+        static_for<0, NMAX>([&](auto i) { v[i] = sh[(uint64_t)((uint32_t)i < n_idx ? i : 0) * B]; });
+        static_for<0, NMAX>([&](auto i) { take(i, v[i]); });
+    } else {                             // wide sets: convert as they land (no i64 copies live)
+        static_for<0, NMAX>([&](auto i) { take(i, sh[(uint64_t)((uint32_t)i < n_idx ? i : 0) * B]); });
+    }
     if (!in_range) {                    // raw i64 shares: exact canonical residues (rare; reloaded)
         const Mod64 PM = make_mod64(P);
         static_for<0, NMAX>([&](auto i) {
