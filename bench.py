@@ -253,8 +253,10 @@ def main():
         if not ok:
             raise SystemExit("combine result check FAILED")
         rows_per_launch = tile if tile else N
-        bytes_per_launch = 8.0 * rows_per_launch * D + 8.0 * D
-        total_bytes = (8.0 * N * D + 8.0 * D * (len(tiles) if tile else 1)) * args.steps * world
+        # one launch reads its rows and writes D results; an accumulating tile launch also reads the
+        # running partial (16 D).  `value` counts the job's own bytes only: N x D shares in, D out.
+        bytes_per_launch = 8.0 * rows_per_launch * D + (16.0 if tile else 8.0) * D
+        total_bytes = (8.0 * N * D + 8.0 * D) * args.steps * world
         value = total_bytes / dt / 1e9
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
         log(f"[combine] rank {rank}: {args.steps} steps in {dt*1e3:.1f} ms, kernel {kernel_ms:.3f} ms "
@@ -533,7 +535,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic_from_profile(tile if tile else N, D)},
             "kernel_ms": round(kernel_ms, 4),
-            "kernel_bytes_per_launch": 8.0 * (tile if tile else N) * D + 8.0 * D,
+            "kernel_bytes_per_launch": bytes_per_launch,
         }
         rec.update(side)
         if world == 1 and not args.no_cpu:
@@ -571,9 +573,9 @@ def traffic_from_profile(N, D):
     path = os.path.join(ROOT, "profiles", "combine_traffic.json")
     try:
         with open(path) as f:
-            t = json.load(f)
-        if t.get("rows") == N and t.get("dim") == D:
-            return t["hbm_bytes_per_launch"]
+            for t in json.load(f)["launches"]:
+                if t.get("rows") == N and t.get("dim") == D:
+                    return t["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         pass
     return None

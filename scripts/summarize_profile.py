@@ -7,7 +7,7 @@ Writes
   profiles/<tag>/kernel_stats.csv      rocprofv3 --kernel-trace --stats summary (same bench command)
   profiles/<tag>/pmc_combine.json      FETCH_SIZE / WRITE_SIZE per combine launch (separate passes)
   profiles/<tag>/bench_traced.json     the bench JSON line printed under the tracer
-  profiles/combine_traffic.json        HBM bytes per combine launch, read by bench.py ("traffic")
+  profiles/combine_traffic.json        HBM bytes per combine launch per (rows, dim), read by bench.py ("traffic")
 HBM bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024: rocprofv3 reports both in KiB, and on gfx950
 FETCH_SIZE counts exactly half of a wide coalesced streaming read (MI355X_MICROARCH.md, HBM).
 """
@@ -38,6 +38,8 @@ def main(tag):
     shutil.copy(os.path.join(src, "bench_traced.json"), os.path.join(dst, "bench_traced.json"))
     bench = json.loads(open(os.path.join(src, "bench_traced.json")).read().strip().splitlines()[-1])
     rows, dim = bench["config"]["participations_per_gpu"], bench["config"]["dim"]
+    tile = bench["config"].get("tile_rows")
+    rows = tile or rows
 
     fetch = pmc_values(os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE",
                        "combine_exact_kernel")
@@ -45,7 +47,7 @@ def main(tag):
                        "combine_exact_kernel")
     f_kib, w_kib = statistics.median(fetch), statistics.median(write)
     hbm = 2 * f_kib * 1024 + w_kib * 1024
-    algo = 8.0 * rows * dim + 8.0 * dim
+    algo = 8.0 * rows * dim + (16.0 if tile else 8.0) * dim      # a tile launch also reads its partial
     # the headline launches: combine dispatches of the rows x dim matrix (the codec leg's smaller
     # combines share the kernel; they are the short ones and are left out)
     with open(os.path.join(src, "trace", "run_kernel_trace.csv")) as f:
@@ -61,9 +63,15 @@ def main(tag):
            "note": "FETCH_SIZE doubled (gfx950 counts half of wide streaming reads); separate --pmc passes"}
     with open(os.path.join(dst, "pmc_combine.json"), "w") as f:
         json.dump(pmc, f, indent=1)
-    with open(os.path.join(ROOT, "profiles", "combine_traffic.json"), "w") as f:
-        json.dump({"rows": rows, "dim": dim, "hbm_bytes_per_launch": hbm, "source": f"profiles/{tag}/pmc_combine.json"},
-                  f, indent=1)
+    path = os.path.join(ROOT, "profiles", "combine_traffic.json")
+    try:
+        launches = json.load(open(path))["launches"]
+    except (OSError, ValueError, KeyError):
+        launches = []
+    launches = [t for t in launches if (t.get("rows"), t.get("dim")) != (rows, dim)]
+    launches.append({"rows": rows, "dim": dim, "hbm_bytes_per_launch": hbm, "source": f"profiles/{tag}/pmc_combine.json"})
+    with open(path, "w") as f:
+        json.dump({"launches": launches}, f, indent=1)
     print(json.dumps(pmc, indent=1))
 
 
