@@ -2,14 +2,15 @@
 """VALU issue roofline of the integer kernels: their instruction mix priced at the measured issue
 rates of tools/ubench_int, combined with the PMC instruction counts of one round.
 
-    python scripts/valu_mix.py <ubench_int.txt> <kernel_report.json> > profiles/valu_roofline.json
+    python scripts/valu_mix.py <ubench_int.txt> <kernel_report.json> [more reports] > profiles/valu_roofline.json
 
 1. The device code of each kernel is compiled with the Makefile's flags (--cuda-device-only) and
    disassembled; every VALU instruction is priced by its class's measured rate (T lane-instr/s):
    the mix ceiling = n_valu / sum(n_class / rate_class) is the lane-op rate the kernel would reach if
    it issued VALU back to back with nothing else in its way (its instruction-mix roofline).
 2. kernel_report.json (scripts/kernel_report.py) gives SQ_INSTS_VALU per launch at the bench
-   configuration (PMC); bench.py divides insts x 64 by the live kernel time and by the ceiling.
+   configuration (PMC; with several reports, a later one overrides an earlier one's kernels);
+   bench.py divides insts x 64 by the live kernel time and by the ceiling.
 """
 import collections
 import json
@@ -109,7 +110,11 @@ def disasm(src, define, frag):
 
 def main():
     R = rates(sys.argv[1])
-    report = json.load(open(sys.argv[2])) if len(sys.argv) > 2 else {}
+    report, sources = {}, {}
+    for path in sys.argv[2:]:
+        for k, v in json.load(open(path)).items():
+            report[k] = v
+            sources[k] = os.path.relpath(path, ROOT)
     out = {"method": __doc__.strip().split("\n\n")[0], "ubench": os.path.relpath(sys.argv[1], ROOT), "kernels": {}}
     for key, src, define, frag in KERNELS:
         name, ops = disasm(src, define, frag)
@@ -122,11 +127,12 @@ def main():
             classes[cls] += c
         rec = {"symbol": name, "static_valu": n, "mix_ceiling_T_lane_ops": round(n / t, 3),
                "classes": dict(classes.most_common())}
-        pmc = next((v for k, v in report.items() if k.endswith(PMC_NAMES[key])), {})
-        c = pmc.get("counters_max_dispatch", {})
+        hit = next((k for k in report if k.endswith(PMC_NAMES[key])), None)
+        c = report[hit].get("counters_max_dispatch", {}) if hit else {}
         if "SQ_INSTS_VALU" in c:
             rec["pmc_valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
             rec["pmc_waves"] = c.get("SQ_WAVES")
+            rec["pmc_source"] = sources[hit]
         out["kernels"][key] = rec
     json.dump(out, sys.stdout, indent=1)
 

@@ -166,6 +166,44 @@ struct Trunc {
     }
 };
 
+// Sign-bit logic for the reveal's lazy path: only bit 31 of each operand matters (a sign).
+//   maj3(a, b, c)    = MAJ(a, b, c)      one v_bitop3_b32
+//   maj3_nb(a, b, c) = MAJ(a, ~b, c)
+__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+__device__ __forceinline__ uint32_t maj3_nb(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xB2);
+}
+
+// Running unsigned min of canonical residues, two per v_min3_u32 (opaque asm, as Trunc): the
+// reveal's sign-bit path is exact unless some residue it produced is 0 (probability ~1/p each).
+struct ZeroTrap {
+    uint32_t zmin = 0xFFFFFFFFu;
+    uint32_t pend = 0;
+    bool has_pend = false;
+    __device__ __forceinline__ void note2(uint32_t a, uint32_t b) {
+        asm("v_min3_u32 %0, %0, %1, %2" : "+v"(zmin) : "v"(a), "v"(b));
+    }
+    __device__ __forceinline__ void note1(uint32_t a) {
+        if (has_pend) {
+            note2(pend, a);
+            has_pend = false;
+        } else {
+            pend = a;
+            has_pend = true;
+        }
+    }
+    __device__ __forceinline__ void flush() {     // call where a runtime branch joins: keeps has_pend constant
+        if (has_pend) note2(pend, pend);
+        has_pend = false;
+    }
+    __device__ __forceinline__ bool bad() {
+        flush();
+        return zmin == 0;
+    }
+};
+
 // Montgomery product with a uniform (SGPR) multiplier as a fixed instruction sequence:
 // v_mad_u64_u32 (T = a' x [+ acc]), v_mul_lo_u32 (u = T pinv), v_mad_u64_u32 (T + u p) -> high word
 // in [0, 2p).  (Left to isel, the exact kernel's lazy variant grew a dead mov + mad-by-0 after

@@ -73,17 +73,95 @@ __device__ __forceinline__ bool load_points(const int64_t* __restrict__ sh, uint
 
 // tss reconstruct of one batch from its m points (shares in (-p, p)): Newton divided differences,
 // then newton_evaluate at omega_secrets^(e+1), e < k; secrets e < lim go to dst[e].  With LAZY
-// (lazy truncation, packed_common.h: Trunc) returns whether the -p trap fired, in which case dst
-// holds garbage and the caller reruns the batch with LAZY = false (tss' `%` verbatim).
+// (the sign-bit formulation below) returns whether a zero residue appeared, in which case dst may
+// hold garbage and the caller reruns the batch with LAZY = false (tss' `%` verbatim).
 // KU > 0: the evaluation loop over the k <= KU secrets is unrolled (table offsets become
 // compile-time constants: merged scalar loads, no per-secret loop overhead).
 // FULL: m == MMAX, so every `i < m` guard is a compile-time constant: no per-step uniform branches,
 // and the table rows load as merged s_load_dwordx16.
+//
+// LAZY: the sign-bit formulation.  A value is kept as its canonical residue c and a word whose bit 31
+// is its sign n (value = c - p n; c = 0 implies n = 0).  Then both of tss' truncations are sign logic:
+//   Newton step  sgn(s_i - s_{i-1}) = MAJ(n_i, ~n_{i-1}, [c_i < c_{i-1}])
+//   fold step    x = acc + t with acc = (pc, n), t = (tc, sgn s xor sgn np):  y = pc + tc in [0, 2p),
+//                sgn(x) = MAJ(n, sgn t, [y < p]) and pc' = y mod p
+// (one v_bitop3 each) -- exact whenever no residue on the way is 0 (then tss gives 0 where the logic
+// may say "negative"); ZeroTrap flags those batches (probability ~1/p per value) for the exact rerun.
+template <int MMAX, int KU, bool FULL>
+__device__ __forceinline__ bool newton_reveal_signbit(FE (&s)[MMAX], uint32_t m, uint32_t k,
+                                                      const uint32_t* __restrict__ tab, const MontP& M, int64_t* dst,
+                                                      uint32_t lim) {
+    const uint32_t p = M.p;
+    ZeroTrap zt;
+    auto newton_step = [&](auto i, uint32_t j) {
+        const uint32_t a_m = tab[OFF_INVM + j * TS + i];
+        uint32_t fc, n;
+        if constexpr (i == 1) {          // (s_1 - s_0) with s_0 = 0, the inserted point (1, 0)
+            fc = montu<false>(a_m, s[1].c, M);
+            n = (uint32_t)s[1].s;
+        } else {
+            const uint32_t d = s[i].c - s[i - 1].c;                    // bit 31: c_i < c_{i-1}
+            fc = montu<false>(a_m, d + p, M);                          // d + p in (0, 2p): REDC input < pR
+            n = maj3_nb((uint32_t)s[i].s, (uint32_t)s[i - 1].s, d);
+        }
+        s[i] = FE{(int32_t)n, fc};
+        zt.note1(fc);
+    };
+    if constexpr (MMAX <= 16) {
+        static_for<1, MMAX>([&](auto j) {
+            if (FULL || (uint32_t)j < m) {
+                static_for<0, MMAX - j>([&](auto ii) {
+                    constexpr int i = MMAX - 1 - ii;
+                    if (FULL || (uint32_t)i < m) newton_step(std::integral_constant<int, i>{}, (uint32_t)j);
+                });
+            }
+        });
+    } else {
+        for (uint32_t j = 1; j < m; ++j) {
+            static_for<0, MMAX - 1>([&](auto ii) {
+                constexpr int i = MMAX - 1 - ii;
+                if ((uint32_t)i < m && (uint32_t)i >= j) newton_step(std::integral_constant<int, i>{}, j);
+            });
+        }
+    }
+    // newton_evaluate: coefficient 0 is the inserted point's value 0, so the fold starts at i = 1
+    auto eval = [&](uint32_t e) {
+        const uint32_t* np = tab + OFF_NP + e * TS;
+        const uint32_t* npm = tab + OFF_NPM + e * TS;
+        uint32_t pc = 0, n = 0;
+        static_for<1, MMAX>([&](auto i) {
+            if (FULL || (uint32_t)i < m) {
+                const uint32_t tc = montu<false>(npm[i], s[i].c, M);
+                const uint32_t st = (uint32_t)s[i].s ^ np[i];               // bit 31: sign of s_i np_i
+                if constexpr (i == 1) {
+                    pc = tc;
+                    n = st;
+                } else {                         // (pc at i = 1 is c_1's product: 0 only if c_1 is)
+                    const uint32_t y = pc + tc;
+                    const uint32_t d = y - p;                               // bit 31: y < p
+                    pc = min(y, d);
+                    n = maj3(n, st, d);
+                    zt.note1(pc);
+                }
+            }
+        });
+        zt.flush();
+        if (e < lim) dst[e] = (int32_t)(pc - (p & (uint32_t)((int32_t)n >> 31)));     // batched.rs:94
+    };
+    if constexpr (KU > 0) {
+        static_for<0, KU>([&](auto e) { if ((uint32_t)e < k) eval((uint32_t)e); });
+    } else {
+        for (uint32_t e = 0; e < k; ++e) eval(e);
+    }
+    return zt.bad();
+}
+
 template <int MMAX, int KU, bool LAZY, bool FULL>
 __device__ __forceinline__ bool newton_reveal(FE (&s)[MMAX], uint32_t m, uint32_t k, const uint32_t* __restrict__ tab,
                                               const MontP& M, int64_t* dst, uint32_t lim) {
+    if constexpr (LAZY) return newton_reveal_signbit<MMAX, KU, FULL>(s, m, k, tab, M, dst, lim);
     const uint32_t p = M.p;
-    Trunc<LAZY> tr;
+    Trunc<false> tr;
     // numtheory::compute_newton_coefficients: for j in 1..m { for i in (j..m).rev() {
     //   s[i] = (((s[i] - s[i-1]) % p) * inv(points[i] - points[i-j])) % p } }
     // inv >= 0, so the product has the sign of the exact difference (or is 0).
@@ -113,9 +191,6 @@ __device__ __forceinline__ bool newton_reveal(FE (&s)[MMAX], uint32_t m, uint32_
             });
         }
     }
-    // LAZY: -(p if coefficient i is negative else 0), hoisted out of the e loop
-    uint32_t nsp[LAZY ? MMAX : 1];
-    if constexpr (LAZY) static_for<0, MMAX>([&](auto i) { nsp[i] = 0u - (p & (uint32_t)(s[i].s >> 31)); });
     // numtheory::newton_evaluate at omega_secrets^(e+1): fold((a + (coef * np) % p) % p)
     auto eval = [&](uint32_t e) {
         const uint32_t* np = tab + OFF_NP + e * TS;
@@ -124,13 +199,7 @@ __device__ __forceinline__ bool newton_reveal(FE (&s)[MMAX], uint32_t m, uint32_
         static_for<0, MMAX>([&](auto i) {
             if (FULL || (uint32_t)i < m) {
                 const uint32_t tc = montu<false>(npm[i], s[i].c, M);
-                // sign of s * np (np != 0 mod p; s == 0 makes tc == 0, exact unless LAZY, whose trap
-                // then sends the batch to the rerun).  LAZY: tc - p [sgn(s) xor sgn(np)]: with both
-                // terms in {0, -p}, -(a xor b) == (-a) xor (-b), so it is one v_xad_u32 of the hoisted
-                // per-coefficient term and the uniform per-table-entry one.
-                int32_t ts;
-                if constexpr (LAZY) ts = (int32_t)((nsp[i] ^ (0u - (p & (uint32_t)((int32_t)np[i] >> 31)))) + tc);
-                else ts = tr(tc, (uint32_t)s[i].s ^ np[i], p);
+                const int32_t ts = tr(tc, (uint32_t)s[i].s ^ np[i], p);     // sign of s * np (np != 0 mod p)
                 const uint32_t ac = addm(acc.c, tc, p);
                 acc = FE{tr(ac, (uint32_t)__builtin_elementwise_add_sat(acc.s, ts), p), ac};
                 tr.note2(ts, acc.s);
@@ -146,7 +215,7 @@ __device__ __forceinline__ bool newton_reveal(FE (&s)[MMAX], uint32_t m, uint32_
     return tr.bad(p);
 }
 
-// One lane = one batch.  LAZY (p >= kLazyTruncMinP): lazy truncation with the -p trap.  A lane whose
+// One lane = one batch.  LAZY (p >= kLazyTruncMinP): the sign-bit path with its zero trap.  A lane whose
 // batch hit the trap (probability ~1/p per value) or has a share outside (-p, p) (raw i64 input) logs
 // the batch and stores garbage; packed_reveal_fixup_kernel, launched right after on the same stream,
 // recomputes the logged batches (exact truncation in registers, or the generic i64 path).  Keeping

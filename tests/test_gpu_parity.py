@@ -417,3 +417,79 @@ def test_packed_reconstruct_traps(engine, oracle, sch):
         rc, exp = oracle.packed_reconstruct(_pp(oracle, sch), D, idx, sh)
         assert rc == 0
         assert_same(got, exp)
+
+
+def _reveal_points(sch, idx):
+    p, wn = sch.prime_modulus, sch.omega_shares
+    return [1] + [pow(wn, i + 1, p) for i in idx]         # packed::reconstruct inserts (1, 0) first
+
+
+def _newton_values(C, xs, p):
+    """Values at xs[1:] of the Newton-form polynomial with coefficients C over the nodes xs."""
+    out = []
+    for xj in xs[1:]:
+        acc, basis = 0, 1
+        for l, c in enumerate(C):
+            acc = (acc + c * basis) % p
+            basis = basis * (xj - xs[l]) % p
+        out.append(acc)
+    return out
+
+
+@pytest.mark.parametrize("sch", [s for s in packed_schemes() if s.prime_modulus >= 2**24 and
+                                 s.secret_count <= 8 and s.reconstruction_threshold() <= 15],
+                         ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")
+def test_packed_reconstruct_zero_residues(engine, oracle, sch):
+    """The sign-bit reveal path is exact unless a residue on the way is 0 mod p; those batches must be
+    caught and recomputed.  Planted per batch, with random signs on the shares:
+      (a) a newton_evaluate partial sum = 0 mod p (the fold's exact value then is 0 or +-p), at a
+          random secret e and step i (i = last: the secret itself is 0 mod p);
+      (b) a divided difference over a random window = 0 mod p (its Newton step's exact difference
+          is 0 or +-p)."""
+    p, n, k = sch.prime_modulus, sch.share_count, sch.secret_count
+    ws = sch.omega_secrets
+    rng = np.random.default_rng(p % 7919 + n)
+    size = min(n, 15)
+    idx = rng.permutation(n)[:size].tolist()
+    xs = _reveal_points(sch, idx)
+    m = size + 1
+    B = 240
+    sh = np.zeros((size, B), np.int64)
+    for b in range(B):
+        if b % 2 == 0:                                   # (a) zero partial sum of the fold
+            e = int(rng.integers(0, k))
+            i = int(rng.integers(2, m)) if b % 6 else m - 1
+            X = pow(ws, e + 1, p)
+            npb = [1]
+            for l in range(m - 1):
+                npb.append(npb[-1] * (X - xs[l]) % p)
+            C = [0] + [int(v) for v in rng.integers(1, p, size=m - 1)]
+            part = sum(C[l] * npb[l] for l in range(1, i)) % p
+            C[i] = (-part) * pow(npb[i], -1, p) % p
+            if C[i] == 0:
+                C[i] = 1
+            y = _newton_values(C, xs, p)
+        else:                                            # (b) zero divided difference over a window
+            L = int(rng.integers(2, m))                  # window of L + 1 nodes: a Newton level L step
+            a = int(rng.integers(0, m - L))
+            y = [int(v) for v in rng.integers(0, p, size=m - 1)]
+            nodes = list(range(a, a + L + 1))
+            w = []
+            for q in nodes:
+                d = 1
+                for r in nodes:
+                    if r != q:
+                        d = d * (xs[q] - xs[r]) % p
+                w.append(pow(d, -1, p))
+            vals = [0] + y                                # node 0 carries value 0
+            s = sum(w[j] * vals[q] for j, q in enumerate(nodes[:-1])) % p
+            last = nodes[-1]
+            vals[last] = (-s) * pow(w[-1], -1, p) % p
+            y = vals[1:]
+        neg = rng.random(size) < 0.5
+        sh[:, b] = [(v - p) if (ng and v) else v for v, ng in zip(y, neg)]
+    D = B * k
+    got = engine.secret_reconstruct(sch, D, [(i, sh[j]) for j, i in enumerate(idx)])
+    rc, exp = oracle.packed_reconstruct(_pp(oracle, sch), D, idx, sh)
+    assert rc == 0
+    assert_same(got, exp)
