@@ -32,18 +32,27 @@ constexpr uint64_t kRegionBytes = kSubBytes * kWPT;
 
 
 
+// Inclusive prefix sum over the 64 lanes of a wave with DPP (row shifts, then the row broadcasts of
+// gfx9): six VALU adds, no LDS round trips.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return x;
+}
+
+// Bits 7, 15, 23, 31 of d -> bits 0..3: the product of the masked word with 2^0 + 2^7 + 2^14 + 2^21
+// moves bit 8k+7 to 28+k; every other partial product lands on a distinct lower bit (no carries).
+__device__ __forceinline__ uint32_t msb_nibble(uint32_t d) {
+    return ((d & 0x80808080u) * 0x00204081u) >> 28;
+}
+
 // 16 bytes as a 16-bit mask of "continuation" bytes (bit j = byte j has 0x80).
 __device__ __forceinline__ uint32_t cont_mask(uint4 w) {
-    uint32_t m = 0;
-    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t hb = d[q] & 0x80808080u;
-        // gather bits 7, 15, 23, 31 into bits 0..3
-        const uint32_t g = (hb >> 7) | (hb >> 14) | (hb >> 21) | (hb >> 28);
-        m |= (g & 0xFu) << (4 * q);
-    }
-    return m;
+    return msb_nibble(w.x) | (msb_nibble(w.y) << 4) | (msb_nibble(w.z) << 8) | (msb_nibble(w.w) << 12);
 }
 
 __device__ __forceinline__ uint8_t byte_of(const uint4& w, int j) {
@@ -56,16 +65,12 @@ __device__ __forceinline__ uint8_t byte_of(const uint4& w, int j) {
 //   term   bit j: a terminator (no 0x80) inside the blob, or the blob's last byte (truncated tail)
 //   cont   bit j: a continuation byte inside the blob (bytes outside the blob count as neither)
 struct Window {
-    uint4 prev, own;
     uint32_t valid, term, cont;
 };
 
-__device__ __forceinline__ Window make_window(uint4 prev, uint4 own, uint64_t word, uint64_t begin, uint64_t end) {
+__device__ __forceinline__ Window make_window_cm(uint32_t cm, uint64_t word, uint64_t begin, uint64_t end) {
     Window W;
     const uint64_t a0 = word * 16;                      // byte offset of own word (aligned)
-    W.own = own;
-    W.prev = prev;
-    const uint32_t cm = cont_mask(W.prev) | (cont_mask(W.own) << 16);
     // window byte j sits at a0 - 16 + j
     uint32_t in = 0;
     {
@@ -80,6 +85,17 @@ __device__ __forceinline__ Window make_window(uint4 prev, uint4 own, uint64_t wo
         W.cont = cm & in;
         W.term = (~cm & in) | (lastbit & in);
     }
+    return W;
+}
+__device__ __forceinline__ Window make_window(uint4 prev, uint4 own, uint64_t word, uint64_t begin, uint64_t end) {
+    return make_window_cm(cont_mask(prev) | (cont_mask(own) << 16), word, begin, end);
+}
+// A window whose 32 bytes all lie inside the blob, with the blob's last byte beyond it.
+__device__ __forceinline__ Window interior_window(uint32_t cm) {
+    Window W;
+    W.valid = 0xFFFF0000u;
+    W.cont = cm;
+    W.term = ~cm;
     return W;
 }
 
@@ -191,26 +207,35 @@ __device__ __forceinline__ uint64_t leb_pack8(uint64_t x) {
     return x;
 }
 
-// pass C: decode.  The region's bytes (plus a 16-byte halo on each side) are staged in LDS; the
-// region is walked as kWPT sub-regions of one word per thread.  Per sub-region a block-wide scan
-// of the terminator counts compacts the elements' (start, length) into LDS; then lane i decodes
-// element i (balanced work, coalesced stores) from three funnel-shifted dwords.  Element index of a terminator = region base + terminators before it in
-// the region.  Blobs flagged irregular are skipped here (varint_sequential_kernel).
+// pass C: decode.  The region's bytes (plus a 16-byte halo on each side) are staged in LDS, with
+// each word's 16-bit continuation mask beside them (so a window's previous-word mask is one LDS
+// read).  The region is walked as kWPT sub-regions of one word per thread.  Per sub-region a
+// block-wide scan of the terminator counts compacts the elements' (start, length) into LDS; then
+// lane i decodes element i (balanced work, coalesced stores) from funnel-shifted dwords -- elements
+// of <= 5 bytes (every field share below 2^31) on a short 32-bit path, longer ones on the general
+// one.  Element index of a terminator = region base + terminators before it in the region.  Blobs
+// flagged irregular are skipped here (varint_sequential_kernel).
+//
+// OutT = int32_t (the clerk's decode -> combine of field shares, |v| < 2^31): the values are stored
+// narrowed and any value that does not fit sets *wide (the caller then decodes again as i64).
+template <typename OutT>
 __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* __restrict__ bytes,
                                                                  const uint64_t* __restrict__ blob_region,
                                                                  const uint64_t* __restrict__ blob_off, uint32_t y0,
                                                                  const uint64_t* __restrict__ region_base,
                                                                  const uint32_t* __restrict__ blob_irregular,
-                                                                 int64_t* __restrict__ out, uint64_t out_stride) {
+                                                                 OutT* __restrict__ out, uint64_t out_stride,
+                                                                 uint32_t* __restrict__ wide) {
     uint32_t b;
     uint64_t r, word;
     if (!region_of(blob_region, blob_off, y0, &b, &r, &word) || blob_irregular[b]) return;
     __shared__ uint32_t lb[(kRegionBytes + 32) / 4];          // [halo 16 B | region 16 KiB | tail 16 B]
+    __shared__ uint32_t cml[kWPT * kThreads + 1];             // continuation mask of lb word w at [w]
     __shared__ uint32_t wsum[kThreads / 64];
     __shared__ uint32_t el[kSubBytes];                        // one sub-region's elements: start | len << 16
     const uint64_t begin = blob_off[b], end = blob_off[b + 1];
-    // stage the region's words (one coalesced load each) and the halo word before it; the windows
-    // (previous word + own word) are then read back from LDS
+    // every window of the region inside the blob, and the blob's last byte past the region
+    const bool interior = word * 16 >= begin + 16 && end > word * 16 + kRegionBytes;
     {
         const uint4* p = reinterpret_cast<const uint4*>(bytes);
         uint4 v[kWPT];
@@ -219,32 +244,35 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
             const uint64_t wk = word + threadIdx.x + k * kThreads;
             v[k] = wk * 16 < end ? p[wk] : make_uint4(0, 0, 0, 0);
         }
-        if (threadIdx.x == 0)
-            reinterpret_cast<uint4*>(lb)[0] = (word * 16 > begin) ? p[word - 1] : make_uint4(0, 0, 0, 0);
+        if (threadIdx.x == 0) {
+            const uint4 h = (word * 16 > begin) ? p[word - 1] : make_uint4(0, 0, 0, 0);
+            reinterpret_cast<uint4*>(lb)[0] = h;
+            cml[0] = cont_mask(h);
+        }
         if (threadIdx.x == kThreads - 1) reinterpret_cast<uint4*>(lb)[kWPT * kThreads + 1] = make_uint4(0, 0, 0, 0);
 #pragma unroll
-        for (int k = 0; k < kWPT; ++k) reinterpret_cast<uint4*>(lb)[threadIdx.x + k * kThreads + 1] = v[k];
+        for (int k = 0; k < kWPT; ++k) {
+            reinterpret_cast<uint4*>(lb)[threadIdx.x + k * kThreads + 1] = v[k];
+            cml[threadIdx.x + k * kThreads + 1] = cont_mask(v[k]);
+        }
     }
     __syncthreads();
     Window W[kWPT];
 #pragma unroll
     for (int k = 0; k < kWPT; ++k) {
         const uint32_t wl = threadIdx.x + k * kThreads;
-        W[k] = make_window(reinterpret_cast<const uint4*>(lb)[wl], reinterpret_cast<const uint4*>(lb)[wl + 1],
-                           word + wl, begin, end);
+        const uint32_t cm = cml[wl] | (cml[wl + 1] << 16);
+        W[k] = interior ? interior_window(cm) : make_window_cm(cm, word + wl, begin, end);
     }
-    int64_t* dst = out + (uint64_t)b * out_stride + region_base[r];
+    OutT* dst = out + (uint64_t)b * out_stride + region_base[r];
+    bool narrow_fail = false;
     uint32_t base = 0;                                        // elements in earlier sub-regions
 #pragma unroll
     for (int k = 0; k < kWPT; ++k) {
         // 1. compaction: each thread lists the (start, length) of the elements ending in its word
         const uint32_t tm = W[k].term & W[k].valid;
         const uint32_t n = __builtin_popcount(tm);
-        uint32_t incl = n;                                    // exclusive scan of n over the block
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(incl, o);
-            if ((threadIdx.x & 63) >= (uint32_t)o) incl += t;
-        }
+        const uint32_t incl = wave_incl_scan(n);              // exclusive scan of n over the block
         __syncthreads();                                      // lb visible; el / wsum free for reuse
         if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
         __syncthreads();
@@ -253,36 +281,70 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
             if (w < (threadIdx.x >> 6)) e += wsum[w];
             total += wsum[w];
         }
-        // an element starts after the previous boundary (a terminator or a byte outside the blob)
-        const uint32_t boundary = W[k].term | ~(W[k].term | W[k].cont);
-        uint32_t rem = tm;
-        while (rem) {
-            const int j = __builtin_ctz(rem);
-            rem &= rem - 1;
-            const uint32_t below = boundary & ((1u << j) - 1u);
-            const int st = below ? 32 - __builtin_clz(below) : 0;      // window index of the first byte
-            el[e++] = ((threadIdx.x + k * kThreads) * 16 + st) | ((uint32_t)(j - st + 1) << 16);
+        if (tm) {
+            // the first element starts after the previous boundary (a terminator, or a byte outside
+            // the blob); each later one right after the terminator before it
+            const uint32_t boundary = W[k].term | ~(W[k].term | W[k].cont);
+            const uint32_t pos0 = (threadIdx.x + k * kThreads) * 16;
+            uint32_t rem = tm;
+            const uint32_t below = boundary & ((1u << __builtin_ctz(rem)) - 1u);
+            uint32_t st = below ? 32 - __builtin_clz(below) : 0;      // window index of the first byte
+            do {
+                const uint32_t j = __builtin_ctz(rem);
+                rem &= rem - 1;
+                el[e++] = (pos0 + st) | ((j - st + 1) << 16);
+                st = j + 1;
+            } while (rem);
         }
         __syncthreads();
         // 2. decode: lane i takes element i -> balanced work, coalesced stores
         for (uint32_t i = threadIdx.x; i < total; i += kThreads) {
             const uint32_t P = el[i] & 0xFFFFu;                  // byte position in lb
-            const int len = (int)(el[i] >> 16);                   // 1..11 on regular blobs
+            const uint32_t len = el[i] >> 16;                     // 1..11 on regular blobs
             const uint32_t q = P >> 2, sh = (P & 3) * 8;
-            const uint32_t d0 = lb[q], d1 = lb[q + 1], d2 = lb[q + 2], d3 = lb[q + 3];
-            const uint32_t b0 = __builtin_amdgcn_alignbit(d1, d0, sh), b1 = __builtin_amdgcn_alignbit(d2, d1, sh),
-                           b2 = __builtin_amdgcn_alignbit(d3, d2, sh);
-            uint64_t lo = ((uint64_t)b1 << 32) | b0;
-            if (len < 8) lo &= (1ull << (8 * len)) - 1;
-            uint64_t z = leb_pack8(lo);
-            if (len > 8) {              // groups 8, 9, 10 at shifts 56, 63, 70 & 63 = 6 (Rust release)
-                const uint32_t hb = b2 & ((len >= 11) ? 0xFFFFFFu : (len == 10 ? 0xFFFFu : 0xFFu));
-                z |= ((uint64_t)(hb & 0x7F) << 56) | ((uint64_t)((hb >> 8) & 0x7F) << 63) |
-                     ((uint64_t)((hb >> 16) & 0x7F) << 6);
+            const uint32_t d0 = lb[q], d1 = lb[q + 1], d2 = lb[q + 2];
+            const uint32_t b0 = __builtin_amdgcn_alignbit(d1, d0, sh), b1 = __builtin_amdgcn_alignbit(d2, d1, sh);
+            if constexpr (sizeof(OutT) < 8) {
+                // int32 output: elements of <= 5 bytes whose zigzag value is below 2^32 (anything
+                // else sets *wide and the caller decodes the job as i64)
+                const uint32_t l4 = len < 4 ? len : 4u, cut = 32 - 8 * l4;
+                uint32_t x = ((b0 << cut) >> cut) & 0x7F7F7F7Fu;
+                x = (x & 0x007F007Fu) | ((x >> 1) & ~0x007F007Fu);
+                x = (x & 0x00003FFFu) | ((x >> 2) & ~0x00003FFFu);
+                const uint32_t g4 = len == 5 ? (b1 & 0x7Fu) : 0u;
+                narrow_fail |= len > 5 || g4 > 15;
+                const uint32_t zl = x | (g4 << 28);
+                dst[base + i] = (OutT)((zl >> 1) ^ (0u - (zl & 1u)));
+                continue;
             }
-            dst[base + i] = (int64_t)((z >> 1) ^ (0 - (z & 1)));
+            int64_t val;
+            if (len <= 5) {
+                // bytes 0..3 (masked to the element) -> 4 x 7-bit groups: two bit-field merges
+                const uint32_t l4 = len < 4 ? len : 4u, cut = 32 - 8 * l4;
+                uint32_t x = ((b0 << cut) >> cut) & 0x7F7F7F7Fu;
+                x = (x & 0x007F007Fu) | ((x >> 1) & ~0x007F007Fu);  // byte pairs -> 14-bit lanes (bit 15 junk)
+                x = (x & 0x00003FFFu) | ((x >> 2) & ~0x00003FFFu);  // -> 28 bits (bits 28..31 clear)
+                const uint32_t g4 = len == 5 ? (b1 & 0x7Fu) : 0u;   // group 4 at bit 28
+                const uint32_t zl = x | (g4 << 28), zh = g4 >> 4;
+                val = (int64_t)((((uint64_t)zh << 32) | zl) >> 1) ^ -(int64_t)(zl & 1u);
+            } else {
+                const uint32_t b2 = __builtin_amdgcn_alignbit(lb[q + 3], d2, sh);
+                uint64_t lo = ((uint64_t)b1 << 32) | b0;
+                if (len < 8) lo &= (1ull << (8 * len)) - 1;
+                uint64_t z = leb_pack8(lo);
+                if (len > 8) {          // groups 8, 9, 10 at shifts 56, 63, 70 & 63 = 6 (Rust release)
+                    const uint32_t hb = b2 & ((len >= 11) ? 0xFFFFFFu : (len == 10 ? 0xFFFFu : 0xFFu));
+                    z |= ((uint64_t)(hb & 0x7F) << 56) | ((uint64_t)((hb >> 8) & 0x7F) << 63) |
+                         ((uint64_t)((hb >> 16) & 0x7F) << 6);
+                }
+                val = (int64_t)((z >> 1) ^ (0 - (z & 1)));
+            }
+            dst[base + i] = (OutT)val;
         }
         base += total;
+    }
+    if constexpr (sizeof(OutT) < 8) {
+        if (narrow_fail) atomicOr(wide, 1u);             // rare: one atomic per lane that saw it
     }
 }
 
@@ -355,20 +417,25 @@ __device__ __forceinline__ uint64_t leb_spread8(uint64_t z) {
 }
 
 // write: coalesced loads (element q * 256 + t of the chunk), one block-wide scan of the sizes per
-// q, bytes assembled in LDS at the chunk's global byte offset mod 4 (so LDS dwords line up with
-// global dwords), then dword stores for the interior and byte stores for the two partial ends
-// (shared with the neighbouring chunks).  chunk_off = row offset + exclusive scan of chunk_bytes.
+// q, each element's bytes ORed into a zeroed LDS image of the chunk's output (its 8 + 2 bytes shifted
+// to their byte offset: 2-4 ds_or_b32, no per-byte stores), the image aligned to the chunk's global
+// byte offset mod 16 so that the interior leaves as 16-byte stores; the two partial 16-byte words at
+// the ends (shared with the neighbouring chunks) are written byte-wise.
+// chunk_off = row offset + exclusive scan of chunk_bytes.
 __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* __restrict__ vals, uint64_t len,
                                                                 uint64_t stride, uint32_t chunks,
                                                                 const uint64_t* __restrict__ chunk_off,
                                                                 uint8_t* __restrict__ dst) {
     const uint32_t c = blockIdx.x, row = blockIdx.y;
     const uint64_t e0 = (uint64_t)c * kEncChunk;
-    __shared__ uint32_t buf[(kEncChunk * 10 + 8) / 4];
+    constexpr uint32_t kBufQuads = (kEncChunk * 10 + 32) / 16;      // lead < 16, + the shifted tail dwords
+    __shared__ uint4 buf4[kBufQuads];
     __shared__ uint32_t wsum[kThreads / 64];
-    const uint64_t go = chunk_off[(uint64_t)row * chunks + c];
-    const uint32_t lead = (uint32_t)(go & 3);
-    uint8_t* b8 = reinterpret_cast<uint8_t*>(buf);
+    uint32_t* buf = reinterpret_cast<uint32_t*>(buf4);
+    const uint8_t* b8 = reinterpret_cast<const uint8_t*>(buf4);
+    uint8_t* gdst = dst + chunk_off[(uint64_t)row * chunks + c];
+    const uint32_t lead = (uint32_t)((uintptr_t)gdst & 15);
+    for (uint32_t k = threadIdx.x; k < kBufQuads; k += kThreads) buf4[k] = make_uint4(0, 0, 0, 0);
     int64_t v[kEncPer];
 #pragma unroll
     for (uint32_t q = 0; q < kEncPer; ++q) {
@@ -381,13 +448,9 @@ __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* _
         const bool in = e0 + q * kThreads + threadIdx.x < len;
         const uint64_t z = ((uint64_t)v[q] << 1) ^ (uint64_t)(v[q] >> 63);
         const uint32_t n = in ? varint_size(v[q]) : 0u;
-        uint32_t incl = n;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(incl, o);
-            if ((threadIdx.x & 63) >= (uint32_t)o) incl += t;
-        }
-        __syncthreads();                                     // wsum of the previous q consumed
-        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+        const uint32_t incl = wave_incl_scan(n);
+        __syncthreads();                                     // wsum of the previous q consumed (and, at
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;    // q = 0, the zeroed image visible)
         __syncthreads();
         uint32_t off = base + incl - n, total = 0;
         for (uint32_t w = 0; w < kThreads / 64; ++w) {
@@ -395,24 +458,34 @@ __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* _
             total += wsum[w];
         }
         base += total;
-        // bytes: groups 0..7 from the spread, continuation bit on every byte but the last
-        const uint64_t lo = leb_spread8(z);
-        const uint32_t g8 = (uint32_t)(z >> 56) & 0x7Fu, g9 = (uint32_t)(z >> 63);
-#pragma unroll
-        for (uint32_t i = 0; i < 8; ++i)
-            if (i < n) b8[off + i] = (uint8_t)(i + 1 < n ? (lo >> (8 * i)) | 0x80 : (lo >> (8 * i)) & 0x7F);
-        if (n > 8) b8[off + 8] = (uint8_t)(g8 | (n > 9 ? 0x80u : 0u));
-        if (n > 9) b8[off + 9] = (uint8_t)g9;
+        if (n) {
+            // bytes 0..7: groups 0..7, continuation bit on every byte but the element's last;
+            // bytes 8, 9 (n > 8): groups 8 and 9
+            const uint32_t nc = n - 1;
+            const uint64_t cont = nc >= 8 ? 0x8080808080808080ull : (0x8080808080808080ull & ((1ull << (8 * nc)) - 1));
+            const uint64_t W = leb_spread8(z) | cont;
+            const uint32_t g8 = (uint32_t)(z >> 56) & 0x7Fu, g9 = (uint32_t)(z >> 63);
+            const uint32_t E = n > 8 ? (g8 | (n > 9 ? 0x80u : 0u) | (g9 << 8)) : 0u;
+            const uint32_t sh = (off & 3) * 8, dw = off >> 2;
+            const uint32_t o0 = (uint32_t)W << sh;
+            const uint32_t o1 = (uint32_t)(W >> (32 - sh));                          // sh = 0: W's high word
+            const uint32_t o2 = (uint32_t)(((((uint64_t)E) << 32) | (uint32_t)(W >> 32)) >> (32 - sh));
+            const uint32_t o3 = sh ? E >> (32 - sh) : 0u;
+            atomicOr(&buf[dw], o0);                                                  // ds_or_b32
+            if (o1) atomicOr(&buf[dw + 1], o1);
+            if (o2) atomicOr(&buf[dw + 2], o2);
+            if (o3) atomicOr(&buf[dw + 3], o3);
+        }
     }
     __syncthreads();
     const uint32_t end = base;                               // lead + chunk bytes
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + (go & ~3ull));
-    uint8_t* d8 = dst + (go & ~3ull);
-    const uint32_t nw = (end + 3) / 4;
-    for (uint32_t k = threadIdx.x; k < nw; k += kThreads) {
-        const uint32_t lo = k * 4, hi = lo + 4;
+    uint4* d128 = reinterpret_cast<uint4*>(gdst - lead);
+    uint8_t* d8 = gdst - lead;
+    const uint32_t nq = (end + 15) / 16;
+    for (uint32_t k = threadIdx.x; k < nq; k += kThreads) {
+        const uint32_t lo = k * 16, hi = lo + 16;
         if (lo >= lead && hi <= end) {
-            d32[k] = buf[k];
+            d128[k] = buf4[k];
         } else {
             for (uint32_t i = lo; i < hi; ++i)
                 if (i >= lead && i < end) d8[i] = b8[i];
@@ -468,7 +541,7 @@ void varint_plan(const uint64_t* blob_off, uint64_t n_blobs, VarintPlan* plan) {
 // Layout of the device workspace for the decode passes.
 struct DecodeWork {
     uint32_t* region_count; uint64_t* region_base;
-    uint64_t* blob_off; uint64_t* blob_region; uint32_t* irregular; uint64_t* blob_count;
+    uint64_t* blob_off; uint64_t* blob_region; uint32_t* irregular; uint64_t* blob_count; uint32_t* wide;
 };
 static DecodeWork carve(void* work, size_t R, uint64_t n_blobs) {
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -479,11 +552,12 @@ static DecodeWork carve(void* work, size_t R, uint64_t n_blobs) {
     w.blob_off = (uint64_t*)p; p += up((n_blobs + 1) * 8);
     w.blob_region = (uint64_t*)p; p += up((n_blobs + 1) * 8);
     w.irregular = (uint32_t*)p; p += up(n_blobs * 4);
-    w.blob_count = (uint64_t*)p;
+    w.blob_count = (uint64_t*)p; p += up(n_blobs * 8);
+    w.wide = (uint32_t*)p;
     return w;
 }
 size_t varint_decode_work_bytes(size_t regions, uint64_t n_blobs) {
-    return regions * 12 + (n_blobs + 1) * 16 + n_blobs * 12 + 8 * 256;
+    return regions * 12 + (n_blobs + 1) * 16 + n_blobs * 12 + 8 * 256;    // (7 x 256 B of rounding + flag)
 }
 
 hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
@@ -524,8 +598,9 @@ hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const Va
     hipError_t e;
     for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
         const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
-        hipLaunchKernelGGL(varint_decode_kernel, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s, bytes,
-                           w.blob_region, w.blob_off, (uint32_t)y0, w.region_base, w.irregular, out, out_stride);
+        hipLaunchKernelGGL(varint_decode_kernel<int64_t>, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s,
+                           bytes, w.blob_region, w.blob_off, (uint32_t)y0, w.region_base, w.irregular, out, out_stride,
+                           w.wide);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (irregular_any) {
@@ -533,6 +608,26 @@ hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const Va
                            w.blob_off, (uint32_t)n_blobs, w.irregular, w.blob_count, out, out_stride, len);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    return hipSuccess;
+}
+
+hipError_t launch_varint_decode_narrow(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
+                                       int32_t* out, uint64_t out_stride, bool* wide_host, hipStream_t s) {
+    const size_t R = plan.regions;
+    DecodeWork w = carve(work, R, n_blobs);
+    hipError_t e;
+    if ((e = hipMemsetAsync(w.wide, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+    for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
+        const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
+        hipLaunchKernelGGL(varint_decode_kernel<int32_t>, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s,
+                           bytes, w.blob_region, w.blob_off, (uint32_t)y0, w.region_base, w.irregular, out, out_stride,
+                           w.wide);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    uint32_t flag = 0;
+    if ((e = hipMemcpyAsync(&flag, w.wide, sizeof(flag), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    *wide_host = flag != 0;
     return hipSuccess;
 }
 

@@ -10,31 +10,34 @@
 // every lane keeps UNROLL * VEC * 8 bytes in flight; with ~30 waves per CU that covers HBM
 // latency.  Non-temporal loads keep the once-read stream from thrashing L2/MALL.
 //
-// Roofline: HBM.  Algorithmic bytes per launch = 8 * n * dim (read) + 8 * dim (write).
+// Roofline: HBM.  Algorithmic bytes per launch = 8 * n * dim (read) + 8 * dim (write)
+// (4 * n * dim read for the int32 rows of the clerk's decode -> combine).
+#include <stdlib.h>
+
 #include "kernels.h"
 
 namespace sda {
 
 namespace {
 
-template <int VEC> struct vec_t;
-template <> struct vec_t<1> { typedef int64_t type; };
-template <> struct vec_t<2> { typedef int64_t type __attribute__((ext_vector_type(2))); };
-template <> struct vec_t<4> { typedef int64_t type __attribute__((ext_vector_type(4))); };
+template <typename T, int VEC> struct vec_t { typedef T type __attribute__((ext_vector_type(VEC))); };
+template <typename T> struct vec_t<T, 1> { typedef T type; };
 
-template <int VEC>
-__device__ __forceinline__ int64_t lane_of(const typename vec_t<VEC>::type& v, int e) {
-    if constexpr (VEC == 1) { return v; } else { return v[e]; }
+template <typename T, int VEC>
+__device__ __forceinline__ int64_t lane_of(const typename vec_t<T, VEC>::type& v, int e) {
+    if constexpr (VEC == 1) { return (int64_t)v; } else { return (int64_t)v[e]; }
 }
 
 // ACC: continue the recurrence from `out` (a previous combine result, |r| < m) instead of 0 --
 // a clerk job streamed through HBM in row tiles is bit-identical to one pass over all rows.
-template <int VEC, int UNROLL, bool SMALL_M, bool ACC>
-__global__ __launch_bounds__(256) void combine_exact_kernel(const int64_t* __restrict__ in,
+// T: the row element type -- int64_t (the ABI's shares), or int32_t for decoded field shares
+// (the clerk's decode -> combine, whose payload values fit: half the bytes to read).
+template <typename T, int VEC, int UNROLL, bool SMALL_M, bool ACC>
+__global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict__ in,
                                                             uint64_t n, uint64_t n_lanes,
                                                             uint64_t stride,
                                                             int64_t* __restrict__ out, Mod64 M) {
-    typedef typename vec_t<VEC>::type V;
+    typedef typename vec_t<T, VEC>::type V;
     const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= n_lanes) return;
     const V* p = reinterpret_cast<const V*>(in + lane * VEC);
@@ -52,32 +55,33 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const int64_t* __res
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) r[e] = add_trem(r[e], lane_of<VEC>(v[u], e), M, SMALL_M);
+            for (int e = 0; e < VEC; ++e) r[e] = add_trem(r[e], lane_of<T, VEC>(v[u], e), M, SMALL_M);
     }
     for (; i < n; ++i) {
         V v = __builtin_nontemporal_load(p);
         p += vstride;
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) r[e] = add_trem(r[e], lane_of<VEC>(v, e), M, SMALL_M);
+        for (int e = 0; e < VEC; ++e) r[e] = add_trem(r[e], lane_of<T, VEC>(v, e), M, SMALL_M);
     }
-    V o;
+    typedef typename vec_t<int64_t, VEC>::type VO;
+    VO o;
     if constexpr (VEC == 1) { o = r[0]; } else {
 #pragma unroll
         for (int e = 0; e < VEC; ++e) o[e] = r[e];
     }
-    reinterpret_cast<V*>(out)[lane] = o;
+    reinterpret_cast<VO*>(out)[lane] = o;
 }
 
-template <int VEC, int UNROLL, bool ACC>
-hipError_t launch_vec(const int64_t* in, uint64_t n, uint64_t dim, uint64_t stride, int64_t* out,
+template <typename T, int VEC, int UNROLL, bool ACC>
+hipError_t launch_vec(const T* in, uint64_t n, uint64_t dim, uint64_t stride, int64_t* out,
                       const Mod64& M, bool small_m, hipStream_t s) {
     const uint64_t n_lanes = dim / VEC;
     const uint64_t blocks = (n_lanes + 255) / 256;
     if (small_m)
-        hipLaunchKernelGGL((combine_exact_kernel<VEC, UNROLL, true, ACC>), dim3((unsigned)blocks), dim3(256), 0, s,
+        hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, true, ACC>), dim3((unsigned)blocks), dim3(256), 0, s,
                            in, n, n_lanes, stride, out, M);
     else
-        hipLaunchKernelGGL((combine_exact_kernel<VEC, UNROLL, false, ACC>), dim3((unsigned)blocks), dim3(256), 0, s,
+        hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, false, ACC>), dim3((unsigned)blocks), dim3(256), 0, s,
                            in, n, n_lanes, stride, out, M);
     return hipGetLastError();
 }
@@ -99,10 +103,27 @@ hipError_t launch_combine_exact(const int64_t* in, uint64_t n, uint64_t dim, uin
     // widest vector whose columns, row stride and base addresses all line up
     const bool v2 = dim % 2 == 0 && stride % 2 == 0 && (a % 16) == 0;
     if (accumulate)
-        return v2 ? launch_vec<2, 8, true>(in, n, dim, stride, out, M, small_m, s)
-                  : launch_vec<1, 8, true>(in, n, dim, stride, out, M, small_m, s);
-    return v2 ? launch_vec<2, 8, false>(in, n, dim, stride, out, M, small_m, s)
-              : launch_vec<1, 8, false>(in, n, dim, stride, out, M, small_m, s);
+        return v2 ? launch_vec<int64_t, 2, 8, true>(in, n, dim, stride, out, M, small_m, s)
+                  : launch_vec<int64_t, 1, 8, true>(in, n, dim, stride, out, M, small_m, s);
+    return v2 ? launch_vec<int64_t, 2, 8, false>(in, n, dim, stride, out, M, small_m, s)
+              : launch_vec<int64_t, 1, 8, false>(in, n, dim, stride, out, M, small_m, s);
+}
+
+hipError_t launch_combine_exact32(const int32_t* in, uint64_t n, uint64_t dim, uint64_t stride,
+                                  int64_t* out, int64_t modulus, hipStream_t s) {
+    if (dim == 0) return hipSuccess;
+    const Mod64 M = make_mod64(modulus);
+    const bool small_m = modulus <= ((int64_t)1 << 62);
+    // 2 columns per lane (8-byte loads: the i64 kernel's grid) or, with SDA_COMBINE32_VEC=4 (A/B knob),
+    // 4 (16-byte loads, half the lanes)
+    const char* env = getenv("SDA_COMBINE32_VEC");
+    const bool want4 = env && atoi(env) == 4;
+    const uintptr_t a = (uintptr_t)in, o = (uintptr_t)out;
+    if (want4 && dim % 4 == 0 && stride % 4 == 0 && a % 16 == 0 && o % 32 == 0)
+        return launch_vec<int32_t, 4, 8, false>(in, n, dim, stride, out, M, small_m, s);
+    const bool v2 = dim % 2 == 0 && stride % 2 == 0 && a % 8 == 0 && o % 16 == 0;
+    return v2 ? launch_vec<int32_t, 2, 8, false>(in, n, dim, stride, out, M, small_m, s)
+              : launch_vec<int32_t, 1, 8, false>(in, n, dim, stride, out, M, small_m, s);
 }
 
 hipError_t launch_mod_canonical(const int64_t* sums, uint64_t dim, int64_t* out, int64_t modulus,

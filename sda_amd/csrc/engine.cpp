@@ -733,6 +733,20 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
     *out_len = dim;
     if (dim == 0) return ok();
     if (sda_status e = ensure(&h->codec_mat, &h->codec_mat_bytes, n_blobs * dim * 8)) return e;
+    // Decoded field shares fit in int32 (|share| < m <= 2^31 for every field the reference uses): the
+    // [N][dim] matrix between the decode and the combine is stored narrowed, which halves its write and
+    // its read.  Any value that does not fit (or a malformed blob) takes the int64 matrix instead.
+    const char* env = getenv("SDA_CODEC_NARROW");                    // "0": A/B and test knob
+    const bool narrow_ok = !(env && atoi(env) == 0);
+    if (narrow_ok && !irregular) {
+        bool wide = false;
+        int32_t* mat32 = static_cast<int32_t*>(h->codec_mat);
+        HIP_TRY(sda::launch_varint_decode_narrow(bytes, n_blobs, plan, h->codec_work, mat32, dim, &wide, st));
+        if (!wide) {
+            HIP_TRY(sda::launch_combine_exact32(mat32, n_blobs, dim, dim, out, mm, st));
+            return SDA_OK;
+        }
+    }
     int64_t* mat = static_cast<int64_t*>(h->codec_mat);
     HIP_TRY(sda::launch_varint_decode(bytes, n_blobs, plan, h->codec_work, mat, dim, dim, irregular, st));
     HIP_TRY(sda::launch_combine_exact(mat, n_blobs, dim, dim, out, mm, st));

@@ -15,6 +15,9 @@ namespace sda {
 // accumulate: continue from the values in `out` (a previous result, |r| < m) instead of 0.
 hipError_t launch_combine_exact(const int64_t* in, uint64_t n, uint64_t dim, uint64_t stride,
                                 int64_t* out, int64_t modulus, hipStream_t s, bool accumulate = false);
+// The same recurrence over int32 rows (decoded field shares: the clerk's decode -> combine).
+hipError_t launch_combine_exact32(const int32_t* in, uint64_t n, uint64_t dim, uint64_t stride,
+                                  int64_t* out, int64_t modulus, hipStream_t s);
 // Canonical residue of u64 sums (multi-GPU finalize).
 hipError_t launch_mod_canonical(const int64_t* sums, uint64_t dim, int64_t* out, int64_t modulus,
                                 hipStream_t s);
@@ -95,6 +98,10 @@ hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_ho
 hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
                                 int64_t* out, uint64_t out_stride, uint64_t len, bool irregular_any,
                                 hipStream_t s);
+// the same decode into int32 (regular blobs only: the caller checked irregular_any == false); *wide_host
+// (synchronous) tells whether some value did not fit, in which case out holds garbage
+hipError_t launch_varint_decode_narrow(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
+                                       int32_t* out, uint64_t out_stride, bool* wide_host, hipStream_t s);
 size_t varint_encode_work_bytes(uint64_t rows, uint64_t len);
 // encode rows [rows][stride] (first len elements) back to back into dst; row_bytes_host gets each
 // row's byte count (synchronous).  hipErrorInvalidValue if dst_cap is too small.

@@ -120,3 +120,35 @@ def test_clerk_decode_combine_dev_and_encode_dev(engine, oracle):
     torch.cuda.synchronize()
     assert n == D
     assert_same(out.cpu().numpy(), oracle.combine(m, xh))
+
+
+@pytest.mark.parametrize("vec", ["2", "4"])
+def test_clerk_decode_combine_narrow_and_wide(engine, oracle, monkeypatch, vec):
+    """The clerk's decode -> combine keeps the decoded matrix as int32 when every value fits (field
+    shares), and falls back to int64 when one does not: both give combiner.rs:16-28's exact result.
+    Edges: -2^31 and 2^31 - 1 fit; 2^31 and -2^31 - 1 do not."""
+    monkeypatch.setenv("SDA_COMBINE32_VEC", vec)
+    m = 2147482801
+    rng = np.random.default_rng(5)
+    N, D = 23, 8004
+    x = rng.integers(-(m - 1), m, size=(N, D), dtype=np.int64)
+    x[3, 5], x[4, 6], x[7, D - 1] = -(2**31), 2**31 - 1, -(2**31)
+    cases = {"fits": x}
+    for name, big in (("above", 2**31), ("below", -(2**31) - 1), ("i64", I64_MIN + 5)):
+        y = x.copy()
+        y[N - 1, D // 2] = big
+        cases[name] = y
+    for name, rows in cases.items():
+        blobs = [oracle.varint_encode(r) for r in rows]
+        t, off = _pack(blobs)
+        out = torch.empty(D, dtype=torch.int64, device="cuda")
+        n = engine.clerk_decode_combine_dev(m, t.data_ptr(), off, out.data_ptr(), D)
+        torch.cuda.synchronize()
+        assert n == D
+        assert_same(out.cpu().numpy(), oracle.combine(m, rows), name)
+        monkeypatch.setenv("SDA_CODEC_NARROW", "0")                      # the int64 path alone
+        out.fill_(7)
+        engine.clerk_decode_combine_dev(m, t.data_ptr(), off, out.data_ptr(), D)
+        torch.cuda.synchronize()
+        assert_same(out.cpu().numpy(), oracle.combine(m, rows), name + " (int64)")
+        monkeypatch.delenv("SDA_CODEC_NARROW")
