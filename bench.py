@@ -180,9 +180,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # one rank per GPU; SDA_DIST_BACKEND=gloo rehearses N ranks on fewer devices (RCCL refuses two
+    # ranks on one device): ranks then share GPUs round-robin, and the collectives run over gloo
+    backend = os.environ.get("SDA_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     eng = Engine(local)
     stream = lambda: torch.cuda.current_stream().cuda_stream   # noqa: E731
     dev = torch.device("cuda", local)
@@ -529,7 +537,8 @@ def main():
                                     "the GPUs, streamed through a resident 1000-row tile (BASELINE.json configs[3])"),
                        "participations_per_gpu": N, "dim": D, "modulus": m,
                        **({"tile_rows": tile, "participations_total": 100_000} if tile else {}),
-                       "parallelism": f"participation split x{world}" + (", RCCL int64 all-reduce" if world > 1 else ""),
+                       "parallelism": f"participation split x{world}" + ((", RCCL int64 all-reduce" if backend == "nccl" else f", {backend} int64 all-reduce (rehearsal)")
+                                                                       if world > 1 else ""),
                        "exact": "combiner.rs:16-28 recurrence, bit-exact"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),

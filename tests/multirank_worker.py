@@ -1,0 +1,78 @@
+"""One rank of tests/test_gpu_multirank.py: the product's multi-GPU helpers (sda_amd.distributed) on the
+HIP engine, two ranks sharing one MI355X (cuda:0) over gloo.
+
+Not a test module: test_gpu_multirank starts two of these as plain child processes (RANK 0 and 1),
+so the collective path of bench.py --gpus N runs with the real device kernels and real device tensors;
+only the transport differs from the 8-GPU node (gloo instead of RCCL, since RCCL refuses two ranks on
+one device).  Rank 0 writes every result to $SDA_MR_OUT (.npz); the parent compares with the oracle.
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# (rows, dim) of the participation-split cases: a ragged small one and a 1000 x 100k block
+CASES = [(37, 129), (1000, 100_003)]
+TILE = 128
+MOD = 2147482801
+SEEDS = (np.arange(48 * 4, dtype=np.int64).reshape(48, 4) * 7919 + 11) % (1 << 31)
+SIGNED = (301, 50_001)
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    torch.cuda.init()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sda_amd import Engine, synth
+    from sda_amd import distributed as Dd
+
+    eng = Engine(0)
+    dev = torch.device("cuda", 0)
+    res = {}
+    for N, D in CASES:
+        s0, cnt = Dd.shard_range(N, rank, world)
+        mine = torch.from_numpy(synth.fill(cnt, D, 0x5DA + 21, 0, MOD, row0=s0)).to(dev)
+        part = torch.empty(D, dtype=torch.int64, device=dev)
+        out = torch.empty(D, dtype=torch.int64, device=dev)
+        Dd.combine_rows_sharded(eng, MOD, mine.data_ptr(), cnt, D, D, part, out)
+        res[f"rows_{N}x{D}"] = out.cpu().numpy()
+        # the same participations streamed as row tiles (configs[3]'s accumulate on every rank)
+        tiles = [(mine[t0].data_ptr(), min(TILE, cnt - t0)) for t0 in range(0, cnt, TILE)]
+        out2 = torch.empty(D, dtype=torch.int64, device=dev)
+        Dd.combine_tiles_sharded(eng, MOD, tiles, D, D, part, out2)
+        res[f"tiles_{N}x{D}"] = out2.cpu().numpy()
+        del mine
+
+    # recipient's ChaCha mask combine, seeds split over the ranks + one reduce
+    s0, cnt = Dd.shard_range(SEEDS.shape[0], rank, world)
+    seeds = torch.from_numpy(SEEDS[s0:s0 + cnt].astype(np.int32)).to(dev)
+    D = 70_001
+    part = torch.empty(D, dtype=torch.int64, device=dev)
+    out = torch.empty(D, dtype=torch.int64, device=dev)
+    Dd.mask_combine_sharded(eng, MOD, D, seeds, part, out)
+    res["mask"] = out.cpu().numpy()
+
+    # signed (order-dependent) combine: column split + all-gather
+    N, D = SIGNED
+    x = torch.from_numpy(synth.fill(N, D, 0x5DA + 22, -(MOD - 1), MOD)).to(dev)
+    full = torch.empty(D, dtype=torch.int64, device=dev)
+    Dd.combine_columns_sharded(eng, MOD, x, full)
+    res["columns"] = full.cpu().numpy()
+
+    torch.cuda.synchronize()
+    dist.barrier()
+    if rank == 0:
+        np.savez(os.environ["SDA_MR_OUT"], **res)
+    dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

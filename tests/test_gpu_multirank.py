@@ -1,0 +1,81 @@
+"""GPU: the multi-GPU helpers (sda_amd.distributed) at world size 2 on the HIP engine.
+
+Two child processes (tests/multirank_worker.py, RANK 0 and 1) share cuda:0 and a gloo process group:
+each runs the engine's device kernels on its own participations / seeds / column slice, and the
+product functions do the exchange (int64 all-reduce + device finalize, or all-gather) on device
+tensors -- the code path of `bench.py --gpus N`, with gloo standing in for RCCL (RCCL refuses two
+ranks on one device; the 8-GPU node runs the same calls over RCCL).  The results must equal the
+reference's single sequential pass (combiner.rs:16-28, chacha.rs:57-76), recomputed by the oracle.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from sda_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import multirank_worker as W  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.fixture(scope="module")
+def results(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("mr") / "res.npz")
+    env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               SDA_MR_OUT=out, PYTHONUNBUFFERED="1")
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "multirank_worker.py")],
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(2)]
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=150)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    with np.load(out) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("N,D", W.CASES)
+def test_world2_rows_and_tiles_equal_single_pass(results, oracle, N, D):
+    """combine_rows_sharded / combine_tiles_sharded: participation split, one int64 all-reduce,
+    device `% m` == the single sequential pass over all N rows."""
+    full = synth.fill(N, D, 0x5DA + 21, 0, W.MOD)
+    exp = oracle.combine(W.MOD, full)
+    assert np.array_equal(results[f"rows_{N}x{D}"], exp)
+    assert np.array_equal(results[f"tiles_{N}x{D}"], exp)
+
+
+def test_world2_mask_combine_seed_split(results, oracle):
+    """mask_combine_sharded: the recipient's ChaCha mask combine over seeds split across ranks."""
+    exp = oracle.chacha_mask_combine(W.MOD, 70_001, W.SEEDS)
+    assert np.array_equal(results["mask"], exp)
+
+
+def test_world2_signed_column_split(results, oracle):
+    """combine_columns_sharded: signed shares (order-dependent exact result), column split +
+    all-gather, bit-exact with the sequential recurrence."""
+    N, D = W.SIGNED
+    x = synth.fill(N, D, 0x5DA + 22, -(W.MOD - 1), W.MOD)
+    exp = oracle.combine(W.MOD, x)
+    assert (exp < 0).any()
+    assert np.array_equal(results["columns"], exp)
