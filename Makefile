@@ -12,7 +12,7 @@ LIB     ?= sda_amd/libsda_engine.so
 
 GEN_PARTS    := 3 9 27 81
 REVEAL_PARTS := 8 16 32 64 96
-PLAIN   := combine elementwise chacha codec snapshot
+PLAIN   := combine elementwise chacha codec snapshot packed_wide
 OBJS    := $(patsubst %,$(OBJDIR)/%.o,$(PLAIN)) $(OBJDIR)/engine.o \
            $(OBJDIR)/packed_gen.o $(patsubst %,$(OBJDIR)/packed_gen_%.o,$(GEN_PARTS)) \
            $(OBJDIR)/packed_reveal.o $(patsubst %,$(OBJDIR)/packed_reveal_%.o,$(REVEAL_PARTS))

@@ -189,7 +189,7 @@ sda_status sda_packed_generate_mode_dev(sda_engine* h, const sda_sharing_scheme*
                                         const int64_t* draws, int64_t* out, int32_t mode, void* stream);
 
 /* Packed-Shamir reveal: shares [n_vectors][n_idx][B] at clerk `indices` (host array),
- * out [n_vectors][dimension].  All n_idx shares are used (batched.rs:75); n_idx <= 95. */
+ * out [n_vectors][dimension].  All n_idx shares are used (batched.rs:75); n_idx <= 1023. */
 sda_status sda_packed_reconstruct_dev(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,
                                       const uint64_t* indices, uint64_t n_idx, uint64_t n_vectors,
                                       const int64_t* shares, int64_t* out, int32_t mode, void* stream);

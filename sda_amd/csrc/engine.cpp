@@ -118,12 +118,12 @@ sda_status check_packed(const sda_sharing_scheme* s) {
     if (n + 1 < k + t + 1)   // tss: vec![0; share_count - reconstruct_limit()] underflows
         return fail(SDA_ERR_PRECONDITION, "share_count (%llu) < secret_count + privacy_threshold (%llu)",
                     (unsigned long long)n, (unsigned long long)(k + t));
-    if (!is_pow(k + t + 1, 2) || k + t + 1 > 64)
-        return fail(SDA_ERR_UNSUPPORTED, "secret_count + privacy_threshold + 1 = %llu must be a power of 2 <= 64",
-                    (unsigned long long)(k + t + 1));
-    if (!is_pow(n + 1, 3) || n + 1 > 81)
-        return fail(SDA_ERR_UNSUPPORTED, "share_count + 1 = %llu must be a power of 3 <= 81",
-                    (unsigned long long)(n + 1));
+    if (!is_pow(k + t + 1, 2) || k + t + 1 > sda::kWideMaxL)
+        return fail(SDA_ERR_UNSUPPORTED, "secret_count + privacy_threshold + 1 = %llu must be a power of 2 <= %u",
+                    (unsigned long long)(k + t + 1), sda::kWideMaxL);
+    if (!is_pow(n + 1, 3) || n + 1 > sda::kWideMaxN3)
+        return fail(SDA_ERR_UNSUPPORTED, "share_count + 1 = %llu must be a power of 3 <= %u",
+                    (unsigned long long)(n + 1), sda::kWideMaxN3);
     if (p < 3 || p % 2 == 0 || p >= ((int64_t)1 << 31))
         return fail(SDA_ERR_UNSUPPORTED, "prime_modulus %lld must be odd and < 2^31 (tss i64 headroom)",
                     (long long)p);

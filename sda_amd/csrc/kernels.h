@@ -43,6 +43,8 @@ struct DeviceTable {
     std::vector<uint8_t> key;
     void* dev = nullptr;
     size_t cap = 0;
+    void* ws = nullptr;           // packed_wide.hip: per-lane transform workspace (grows, never shrinks)
+    size_t ws_cap = 0;
 };
 hipError_t ensure_table(DeviceTable& t, const std::vector<uint8_t>& key, const void* host, size_t bytes);
 void free_table(DeviceTable& t);
@@ -70,15 +72,25 @@ hipError_t launch_packed_generate(const PackedGenArgs& a, uint32_t k, uint32_t t
 struct PackedRevealArgs {
     const int64_t* shares; uint64_t dimension; uint64_t n_vectors; int64_t* out;
 };
-// Reveal takes up to kRevealMaxShares clerk shares per batch (n + 1 <= 81 gives n <= 80 clerks;
-// the kernels keep n_idx + 1 Newton points in registers).
+// The register reveal kernels take up to kRevealMaxPoints - 1 clerk shares per batch (n + 1 <= 81
+// gives n <= 80 clerks; they keep n_idx + 1 Newton points in registers).
 constexpr int kRevealMaxPoints = 96;
-constexpr uint32_t kRevealMaxShares = kRevealMaxPoints - 1;
+// Past these sizes (k + t + 1 > 64, n + 1 > 81, more than kRevealMaxPoints - 1 shares) the packed
+// calls take packed_wide.hip's workspace kernels, up to the engine's domain limits below.
+constexpr uint32_t kWideMaxL = 1024;       // k + t + 1
+constexpr uint32_t kWideMaxN3 = 729;       // n + 1
+constexpr uint32_t kRevealMaxShares = 1023;
+hipError_t launch_packed_generate_wide(const PackedGenArgs& a, uint32_t k, uint32_t t, uint32_t n, uint32_t p,
+                                       uint32_t omega_secrets, uint32_t omega_shares, DeviceTable& tab,
+                                       hipStream_t s);
 // returns hipErrorInvalidValue for CANONICAL mode with duplicate clerk points.  `log_buf`: device
 // memory of packed_gen_log_bytes() bytes (batches the exact kernel hands to its generic fix-up).
 hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indices, uint32_t n_idx, uint32_t k,
                                 uint32_t p, uint32_t omega_secrets, uint32_t omega_shares, int mode,
                                 DeviceTable& tab, void* log_buf, hipStream_t s);
+hipError_t launch_packed_reveal_wide(const PackedRevealArgs& a, const uint64_t* indices, uint32_t n_idx, uint32_t k,
+                                     uint32_t p, uint32_t omega_secrets, uint32_t omega_shares, int mode,
+                                     DeviceTable& tab, hipStream_t s);
 
 // ---- codec.hip (share payload codec: sodium.rs:36-41 / :82-88, integer-encoding 1.0 VarInt) ----
 // Host-side plan of the decode: blobs are split into 4 KiB regions aligned to the (16-byte

@@ -517,6 +517,8 @@ hipError_t launch_packed_generate(const PackedGenArgs& args, uint32_t k, uint32_
     PackedGenArgs a = args;
     a.prime = p;
     const uint32_t L = k + t + 1, N3 = n + 1;
+    if (L > 64 || N3 > 81)                       // past the register kernels: packed_wide.hip
+        return launch_packed_generate_wide(a, k, t, n, p, omega_secrets, omega_shares, tab, s);
     const uint64_t B = (a.dimension + k - 1) / k;
     if (B == 0 || a.n_vectors == 0) return hipSuccess;
     const uint32_t kv[5] = {L, N3, p, omega_secrets, omega_shares};
@@ -563,8 +565,9 @@ hipError_t ensure_table(DeviceTable& t, const std::vector<uint8_t>& key, const v
 
 void free_table(DeviceTable& t) {
     if (t.dev) (void)hipFree(t.dev);
-    t.dev = nullptr;
-    t.cap = 0;
+    if (t.ws) (void)hipFree(t.ws);
+    t.dev = t.ws = nullptr;
+    t.cap = t.ws_cap = 0;
     t.key.clear();
 }
 

@@ -454,6 +454,8 @@ hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indic
                                 DeviceTable& tab, void* log_buf, hipStream_t s) {
     const uint64_t B = (a.dimension + k - 1) / k;
     if (B == 0 || a.n_vectors == 0) return hipSuccess;
+    if ((mode == 0 ? n_idx + 1 : n_idx) > (uint32_t)kRevealMaxPoints || k > (uint32_t)KMAX)   // packed_wide.hip
+        return launch_packed_reveal_wide(a, indices, n_idx, k, p, omega_secrets, omega_shares, mode, tab, s);
     std::vector<uint8_t> key(sizeof(uint32_t) * 6 + sizeof(uint64_t) * n_idx);
     const uint32_t kv[6] = {n_idx, k, p, omega_secrets, omega_shares, (uint32_t)mode};
     memcpy(key.data(), kv, sizeof(kv));

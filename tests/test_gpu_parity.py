@@ -493,3 +493,83 @@ def test_packed_reconstruct_zero_residues(engine, oracle, sch):
     rc, exp = oracle.packed_reconstruct(_pp(oracle, sch), D, idx, sh)
     assert rc == 0
     assert_same(got, exp)
+
+
+# ------------------------------------------------------------------ packed Shamir past the register kernels
+# tss takes any power-of-2 k + t + 1 and power-of-3 n + 1; past 64 / 81 (and past 95 shares per reveal)
+# the engine runs packed_wide.hip's workspace kernels.  (k, t, n): L = 128 / 256 over 243 / 729 points,
+# and a small L over 243 points (reveals from up to 242 shares through the wide Newton path).
+def wide_schemes():
+    out = []
+    for k, t, n in [(100, 27, 242), (64, 63, 242), (5, 2, 242), (200, 55, 728), (1, 0, 242)]:
+        L, N3 = k + t + 1, n + 1
+        p = _prime_for(L, N3)
+        ws, wn = _roots(p, L, N3)
+        out.append(S.PackedShamir(k, n, t, p, ws, wn))
+    return out
+
+
+@pytest.mark.parametrize("sch", wide_schemes(), ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")
+def test_packed_wide_generate(engine, oracle, sch):
+    """Share-gen at k + t + 1 > 64 or n + 1 > 81 == tss (oracle), signed and canonical, raw i64 secrets too."""
+    import torch
+    p, k = sch.prime_modulus, sch.secret_count
+    rng = np.random.default_rng(p % 1009 + sch.share_count)
+    D = 9 * k + 1
+    B = (D + k - 1) // k
+    secrets = rng.integers(-(p - 1), p, size=D, dtype=np.int64)
+    secrets[::5] = rng.integers(-(2**40), 2**40, size=secrets[::5].size, dtype=np.int64)
+    draws = rng.integers(0, p - 1, size=B * sch.privacy_threshold(), dtype=np.int64)
+    exp = oracle.packed_generate(_pp(oracle, sch), secrets, draws)
+    assert_same(engine.share_generate(sch, secrets, draws), exp)
+    ds, dd = torch.as_tensor(secrets).cuda(), torch.as_tensor(draws).cuda()
+    out = torch.empty((2, sch.share_count, B), dtype=torch.int64, device="cuda")
+    dd2 = torch.cat([dd, dd])
+    ds2 = torch.cat([ds, ds])                   # two vectors per launch
+    engine.packed_generate_mode_dev(sch, ds2.data_ptr(), D, 2, dd2.data_ptr(), out.data_ptr(), E.REVEAL_CANONICAL)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert_same(got[0], np.mod(exp, p))
+    assert_same(got[1], np.mod(exp, p))
+
+
+@pytest.mark.parametrize("sch", wide_schemes(), ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")
+def test_packed_wide_reconstruct(engine, oracle, sch):
+    """Reveal from every share (batched.rs:75) and from random subsets, through the register kernels
+    (<= 95 shares) and the wide Newton path (more), both modes, == tss (oracle)."""
+    import torch
+    p, n, k = sch.prime_modulus, sch.share_count, sch.secret_count
+    rng = np.random.default_rng(p % 331 + n)
+    D = 5 * k + 1
+    B = (D + k - 1) // k
+    secrets = rng.integers(0, p, size=D, dtype=np.int64)
+    draws = rng.integers(0, p - 1, size=B * sch.privacy_threshold(), dtype=np.int64)
+    shares = oracle.packed_generate(_pp(oracle, sch), secrets, draws)
+    need = sch.reconstruction_threshold()
+    sizes = [n, max(need, 96), max(need, 95), need] + [int(rng.integers(need, n + 1)) for _ in range(2)]
+    for size in sizes:
+        idx = rng.permutation(n)[:size].tolist()
+        got = engine.secret_reconstruct(sch, D, [(i, shares[i]) for i in idx])
+        rc, exp = oracle.packed_reconstruct(_pp(oracle, sch), D, idx, shares[idx])
+        assert rc == 0
+        assert_same(got, exp)
+        assert (got % p == secrets % p).all()
+        dsh = torch.as_tensor(np.ascontiguousarray(shares[idx])).cuda()
+        out = torch.empty(D, dtype=torch.int64, device="cuda")
+        engine.packed_reconstruct_dev(sch, D, idx, 1, dsh.data_ptr(), out.data_ptr(), mode=E.REVEAL_CANONICAL)
+        torch.cuda.synchronize()
+        assert_same(out.cpu().numpy(), np.mod(exp, p))
+    # shares outside (-p, p): tss' wrapping arithmetic on the wide path as well
+    idx = list(range(max(need, min(n, 120))))
+    raw = shares[idx].copy()
+    raw[0, ::3] += 5 * p
+    got = engine.secret_reconstruct(sch, D, [(i, raw[j]) for j, i in enumerate(idx)])
+    rc, exp = oracle.packed_reconstruct(_pp(oracle, sch), D, idx, raw)
+    assert_same(got, exp)
+
+
+def test_packed_wide_domain_limits(engine):
+    """Past the engine's domain (k + t + 1 > 1024, n + 1 > 729) the call is refused, not approximated."""
+    with pytest.raises(SdaError) as ei:
+        engine.share_generate(S.PackedShamir(1000, 2186, 1047, 2147483647 - 12, 3, 5), [1], [0] * 1047)
+    assert ei.value.status == E.ERR_UNSUPPORTED
