@@ -383,6 +383,13 @@ __device__ __forceinline__ uint32_t varint_size(int64_t v) {
 
 constexpr uint32_t kEncChunk = 2048;          // elements per encode block
 constexpr uint32_t kEncPer = kEncChunk / kThreads;
+constexpr uint32_t kEncPairs = kEncPer / 2;   // rounds of one adjacent element pair per lane
+typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+// A full chunk whose first element is 16-byte aligned is read as element pairs (one 16-byte load per
+// lane: a wave moves 1 KiB per load instruction instead of 512 B).
+__device__ __forceinline__ bool enc_pairs_ok(const int64_t* rowp, uint64_t e0, uint64_t len) {
+    return e0 + kEncChunk <= len && ((uintptr_t)(rowp + e0) & 15) == 0;
+}
 
 // sizes of each [row][chunk] block of elements
 __global__ __launch_bounds__(kThreads) void varint_size_kernel(const int64_t* __restrict__ vals, uint64_t len,
@@ -390,11 +397,20 @@ __global__ __launch_bounds__(kThreads) void varint_size_kernel(const int64_t* __
                                                                uint64_t* __restrict__ chunk_bytes) {
     const uint32_t c = blockIdx.x, row = blockIdx.y;
     const uint64_t e0 = (uint64_t)c * kEncChunk;
+    const int64_t* rowp = vals + (uint64_t)row * stride;
     uint64_t n = 0;
+    if (enc_pairs_ok(rowp, e0, len)) {          // 16-byte loads: element pairs (order is irrelevant here)
 #pragma unroll
-    for (uint32_t q = 0; q < kEncPer; ++q) {
-        const uint64_t e = e0 + q * kThreads + threadIdx.x;
-        if (e < len) n += varint_size(vals[row * stride + e]);
+        for (uint32_t q = 0; q < kEncPairs; ++q) {
+            const i64x2 x = __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(rowp + e0) + q * kThreads + threadIdx.x);
+            n += varint_size(x[0]) + varint_size(x[1]);
+        }
+    } else {
+#pragma unroll
+        for (uint32_t q = 0; q < kEncPer; ++q) {
+            const uint64_t e = e0 + q * kThreads + threadIdx.x;
+            if (e < len) n += varint_size(rowp[e]);
+        }
     }
     __shared__ uint64_t red[kThreads / 64];
     for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
@@ -416,8 +432,8 @@ __device__ __forceinline__ uint64_t leb_spread8(uint64_t z) {
     return x;
 }
 
-// write: coalesced loads (element q * 256 + t of the chunk), one block-wide scan of the sizes per
-// q, each element's bytes ORed into a zeroed LDS image of the chunk's output (its 8 + 2 bytes shifted
+// write: coalesced 16-byte loads (lane t: elements 512 q + 2 t + {0, 1} of the chunk), one block-wide
+// scan of the pair sizes per q, each element's bytes ORed into a zeroed LDS image of the chunk's output (its 8 + 2 bytes shifted
 // to their byte offset: 2-4 ds_or_b32, no per-byte stores), the image aligned to the chunk's global
 // byte offset mod 16 so that the interior leaves as 16-byte stores; the two partial 16-byte words at
 // the ends (shared with the neighbouring chunks) are written byte-wise.
@@ -436,45 +452,64 @@ __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* _
     uint8_t* gdst = dst + chunk_off[(uint64_t)row * chunks + c];
     const uint32_t lead = (uint32_t)((uintptr_t)gdst & 15);
     for (uint32_t k = threadIdx.x; k < kBufQuads; k += kThreads) buf4[k] = make_uint4(0, 0, 0, 0);
-    int64_t v[kEncPer];
+    // round q: lane t owns the adjacent elements e0 + 512 q + 2 t + {0, 1} (one 16-byte load when the
+    // chunk allows it), so one block-wide scan of the pair sizes places 512 elements
+    const int64_t* rowp = vals + (uint64_t)row * stride;
+    int64_t v[kEncPairs][2];
+    if (enc_pairs_ok(rowp, e0, len)) {
 #pragma unroll
-    for (uint32_t q = 0; q < kEncPer; ++q) {
-        const uint64_t e = e0 + q * kThreads + threadIdx.x;
-        v[q] = e < len ? vals[row * stride + e] : 0;
+        for (uint32_t q = 0; q < kEncPairs; ++q) {
+            const i64x2 x = __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(rowp + e0) + q * kThreads + threadIdx.x);
+            v[q][0] = x[0];
+            v[q][1] = x[1];
+        }
+    } else {
+#pragma unroll
+        for (uint32_t q = 0; q < kEncPairs; ++q) {
+            const uint64_t e = e0 + 2 * (q * kThreads + threadIdx.x);
+            v[q][0] = e < len ? rowp[e] : 0;
+            v[q][1] = e + 1 < len ? rowp[e + 1] : 0;
+        }
     }
     uint32_t base = lead;
 #pragma unroll
-    for (uint32_t q = 0; q < kEncPer; ++q) {
-        const bool in = e0 + q * kThreads + threadIdx.x < len;
-        const uint64_t z = ((uint64_t)v[q] << 1) ^ (uint64_t)(v[q] >> 63);
-        const uint32_t n = in ? varint_size(v[q]) : 0u;
-        const uint32_t incl = wave_incl_scan(n);
+    for (uint32_t q = 0; q < kEncPairs; ++q) {
+        const uint64_t e = e0 + 2 * (q * kThreads + threadIdx.x);
+        const uint32_t n0 = e < len ? varint_size(v[q][0]) : 0u;
+        const uint32_t n1 = e + 1 < len ? varint_size(v[q][1]) : 0u;
+        const uint32_t np = n0 + n1;
+        const uint32_t incl = wave_incl_scan(np);
         __syncthreads();                                     // wsum of the previous q consumed (and, at
         if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;    // q = 0, the zeroed image visible)
         __syncthreads();
-        uint32_t off = base + incl - n, total = 0;
+        uint32_t off0 = base + incl - np, total = 0;
         for (uint32_t w = 0; w < kThreads / 64; ++w) {
-            if (w < (threadIdx.x >> 6)) off += wsum[w];
+            if (w < (threadIdx.x >> 6)) off0 += wsum[w];
             total += wsum[w];
         }
         base += total;
-        if (n) {
-            // bytes 0..7: groups 0..7, continuation bit on every byte but the element's last;
-            // bytes 8, 9 (n > 8): groups 8 and 9
-            const uint32_t nc = n - 1;
-            const uint64_t cont = nc >= 8 ? 0x8080808080808080ull : (0x8080808080808080ull & ((1ull << (8 * nc)) - 1));
-            const uint64_t W = leb_spread8(z) | cont;
-            const uint32_t g8 = (uint32_t)(z >> 56) & 0x7Fu, g9 = (uint32_t)(z >> 63);
-            const uint32_t E = n > 8 ? (g8 | (n > 9 ? 0x80u : 0u) | (g9 << 8)) : 0u;
-            const uint32_t sh = (off & 3) * 8, dw = off >> 2;
-            const uint32_t o0 = (uint32_t)W << sh;
-            const uint32_t o1 = (uint32_t)(W >> (32 - sh));                          // sh = 0: W's high word
-            const uint32_t o2 = (uint32_t)(((((uint64_t)E) << 32) | (uint32_t)(W >> 32)) >> (32 - sh));
-            const uint32_t o3 = sh ? E >> (32 - sh) : 0u;
-            atomicOr(&buf[dw], o0);                                                  // ds_or_b32
-            if (o1) atomicOr(&buf[dw + 1], o1);
-            if (o2) atomicOr(&buf[dw + 2], o2);
-            if (o3) atomicOr(&buf[dw + 3], o3);
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t n = h ? n1 : n0, off = h ? off0 + n0 : off0;
+            const uint64_t z = ((uint64_t)v[q][h] << 1) ^ (uint64_t)(v[q][h] >> 63);
+            if (n) {
+                // bytes 0..7: groups 0..7, continuation bit on every byte but the element's last;
+                // bytes 8, 9 (n > 8): groups 8 and 9
+                const uint32_t nc = n - 1;
+                const uint64_t cont = nc >= 8 ? 0x8080808080808080ull : (0x8080808080808080ull & ((1ull << (8 * nc)) - 1));
+                const uint64_t W = leb_spread8(z) | cont;
+                const uint32_t g8 = (uint32_t)(z >> 56) & 0x7Fu, g9 = (uint32_t)(z >> 63);
+                const uint32_t E = n > 8 ? (g8 | (n > 9 ? 0x80u : 0u) | (g9 << 8)) : 0u;
+                const uint32_t sh = (off & 3) * 8, dw = off >> 2;
+                const uint32_t o0 = (uint32_t)W << sh;
+                const uint32_t o1 = (uint32_t)(W >> (32 - sh));                          // sh = 0: W's high word
+                const uint32_t o2 = (uint32_t)(((((uint64_t)E) << 32) | (uint32_t)(W >> 32)) >> (32 - sh));
+                const uint32_t o3 = sh ? E >> (32 - sh) : 0u;
+                atomicOr(&buf[dw], o0);                                                  // ds_or_b32
+                if (o1) atomicOr(&buf[dw + 1], o1);
+                if (o2) atomicOr(&buf[dw + 2], o2);
+                if (o3) atomicOr(&buf[dw + 3], o3);
+            }
         }
     }
     __syncthreads();
