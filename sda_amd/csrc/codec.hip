@@ -383,7 +383,12 @@ __device__ __forceinline__ uint32_t varint_size(int64_t v) {
 
 constexpr uint32_t kEncChunk = 2048;          // elements per encode block
 constexpr uint32_t kEncPer = kEncChunk / kThreads;
-constexpr uint32_t kEncPairs = kEncPer / 2;   // rounds of one adjacent element pair per lane
+constexpr uint32_t kEncPairs = kEncPer / 2;   // size pass: rounds of one adjacent element pair per lane
+#ifndef SDA_ENC_EPL
+#define SDA_ENC_EPL 2
+#endif
+constexpr uint32_t kEncEpl = SDA_ENC_EPL;     // write pass: adjacent elements per lane per round (even)
+constexpr uint32_t kEncRounds = kEncChunk / (kEncEpl * kThreads);
 typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
 // A full chunk whose first element is 16-byte aligned is read as element pairs (one 16-byte load per
 // lane: a wave moves 1 KiB per load instruction instead of 512 B).
@@ -432,8 +437,8 @@ __device__ __forceinline__ uint64_t leb_spread8(uint64_t z) {
     return x;
 }
 
-// write: coalesced 16-byte loads (lane t: elements 512 q + 2 t + {0, 1} of the chunk), one block-wide
-// scan of the pair sizes per q, each element's bytes ORed into a zeroed LDS image of the chunk's output (its 8 + 2 bytes shifted
+// write: coalesced 16-byte loads (lane t: kEncEpl adjacent elements per round q), one block-wide
+// scan of the lane sizes per q, each element's bytes ORed into a zeroed LDS image of the chunk's output (its 8 + 2 bytes shifted
 // to their byte offset: 2-4 ds_or_b32, no per-byte stores), the image aligned to the chunk's global
 // byte offset mod 16 so that the interior leaves as 16-byte stores; the two partial 16-byte words at
 // the ends (shared with the neighbouring chunks) are written byte-wise.
@@ -452,32 +457,40 @@ __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* _
     uint8_t* gdst = dst + chunk_off[(uint64_t)row * chunks + c];
     const uint32_t lead = (uint32_t)((uintptr_t)gdst & 15);
     for (uint32_t k = threadIdx.x; k < kBufQuads; k += kThreads) buf4[k] = make_uint4(0, 0, 0, 0);
-    // round q: lane t owns the adjacent elements e0 + 512 q + 2 t + {0, 1} (one 16-byte load when the
-    // chunk allows it), so one block-wide scan of the pair sizes places 512 elements
+    // round q: lane t owns the kEncEpl adjacent elements e0 + R q + kEncEpl t + j (R = kEncEpl * 256;
+    // 16-byte loads when the chunk allows it), so one block-wide scan of the lane sizes places R elements
     const int64_t* rowp = vals + (uint64_t)row * stride;
-    int64_t v[kEncPairs][2];
+    int64_t v[kEncRounds][kEncEpl];
     if (enc_pairs_ok(rowp, e0, len)) {
 #pragma unroll
-        for (uint32_t q = 0; q < kEncPairs; ++q) {
-            const i64x2 x = __builtin_nontemporal_load(reinterpret_cast<const i64x2*>(rowp + e0) + q * kThreads + threadIdx.x);
-            v[q][0] = x[0];
-            v[q][1] = x[1];
-        }
+        for (uint32_t q = 0; q < kEncRounds; ++q)
+#pragma unroll
+            for (uint32_t j = 0; j < kEncEpl / 2; ++j) {
+                const i64x2 x = __builtin_nontemporal_load(
+                    reinterpret_cast<const i64x2*>(rowp + e0 + kEncEpl * (q * kThreads + threadIdx.x)) + j);
+                v[q][2 * j] = x[0];
+                v[q][2 * j + 1] = x[1];
+            }
     } else {
 #pragma unroll
-        for (uint32_t q = 0; q < kEncPairs; ++q) {
-            const uint64_t e = e0 + 2 * (q * kThreads + threadIdx.x);
-            v[q][0] = e < len ? rowp[e] : 0;
-            v[q][1] = e + 1 < len ? rowp[e + 1] : 0;
-        }
+        for (uint32_t q = 0; q < kEncRounds; ++q)
+#pragma unroll
+            for (uint32_t j = 0; j < kEncEpl; ++j) {
+                const uint64_t e = e0 + kEncEpl * (q * kThreads + threadIdx.x) + j;
+                v[q][j] = e < len ? rowp[e] : 0;
+            }
     }
     uint32_t base = lead;
 #pragma unroll
-    for (uint32_t q = 0; q < kEncPairs; ++q) {
-        const uint64_t e = e0 + 2 * (q * kThreads + threadIdx.x);
-        const uint32_t n0 = e < len ? varint_size(v[q][0]) : 0u;
-        const uint32_t n1 = e + 1 < len ? varint_size(v[q][1]) : 0u;
-        const uint32_t np = n0 + n1;
+    for (uint32_t q = 0; q < kEncRounds; ++q) {
+        const uint64_t e = e0 + kEncEpl * (q * kThreads + threadIdx.x);
+        uint32_t ns[kEncEpl], pre[kEncEpl], np = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kEncEpl; ++j) {
+            ns[j] = e + j < len ? varint_size(v[q][j]) : 0u;
+            pre[j] = np;
+            np += ns[j];
+        }
         const uint32_t incl = wave_incl_scan(np);
         __syncthreads();                                     // wsum of the previous q consumed (and, at
         if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;    // q = 0, the zeroed image visible)
@@ -489,8 +502,8 @@ __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* _
         }
         base += total;
 #pragma unroll
-        for (uint32_t h = 0; h < 2; ++h) {
-            const uint32_t n = h ? n1 : n0, off = h ? off0 + n0 : off0;
+        for (uint32_t h = 0; h < kEncEpl; ++h) {
+            const uint32_t n = ns[h], off = off0 + pre[h];
             const uint64_t z = ((uint64_t)v[q][h] << 1) ^ (uint64_t)(v[q][h] >> 63);
             if (n) {
                 // bytes 0..7: groups 0..7, continuation bit on every byte but the element's last;
