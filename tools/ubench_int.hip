@@ -46,7 +46,11 @@ __global__ __launch_bounds__(256) void ubench(uint32_t seed, uint64_t* sink) {
         if constexpr (OP == 26) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a##i) : "v"(b));        \
         if constexpr (OP == 27) asm volatile("v_add_co_u32 %0, vcc, %0, %1\n\tv_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(a##i) : "v"(b) : "vcc"); \
         if constexpr (OP == 28) asm volatile("v_min_i32 %0, %0, %1" : "+v"(a##i) : "v"(b));            \
-        if constexpr (OP == 29) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a##i));
+        if constexpr (OP == 29) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a##i)); \
+        if constexpr (OP == 30) { uint32_t t_;                                                          \
+            asm volatile("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1\n\t" \
+                         "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0" \
+                         : "=&v"(t_) : "v"(a##i), "v"(b)); a##i = t_; }
         REP8(STEP)
     }
     uint64_t s = (uint64_t)a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + w0 + w1 + w2 + w3 + w4 + w5 + w6 + w7;
@@ -103,6 +107,7 @@ int main() {
     run<25>("v_lshl_or_b32", sink, 1);
     run<26>("v_mul_u32_u24", sink, 1);
     run<27>("v_add_co + v_addc_co", sink, 2);
+    run<30>("v_xor_b32_sdwa x2 (rot16)", sink, 2);
     run<0>("v_add_u32 (again)", sink, 1);
     (void)hipFree(sink);
     return 0;
