@@ -353,6 +353,20 @@ def main():
         ex = side["shamir"].get("gen_exact_valu")
         if ex:      # integer-op throughput of share-gen (north star: "integer-op throughput in rocprof")
             side["shamir"]["int_ops_per_s"] = ex["achieved"] * 1e12
+        if world > 1:
+            # "packed-Shamir shares/s at 1/2/4/8 GPUs": every rank generates its own participants'
+            # shares at once (vector split, no collective); whole-job rate over the max-over-ranks time
+            torch.cuda.synchronize()
+            barrier()
+            t_all = time.perf_counter()
+            for _ in range(args.steps):
+                gen()
+            torch.cuda.synchronize()
+            barrier()
+            tt = torch.tensor([time.perf_counter() - t_all], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            side["shamir"]["shares_per_s_all_gpus"] = world * V * n * B * args.steps / float(tt.item())
+            side["shamir"]["n_gpus"] = world
         log(f"[shamir] {json.dumps(side['shamir'])}")
         del sec, drw, sh, sub, rev
     if not args.no_side and args.only in (None, "chacha"):
