@@ -150,3 +150,24 @@ def test_aggregation_end_to_end_on_device(engine, mode, gen_mode):
     torch.cuda.synchronize()
     assert L == D
     assert_same(out.cpu().numpy(), inputs.sum(axis=0) % P)
+
+
+def test_recipient_reveal_wide_scheme(engine):
+    """The recipient pipeline over a scheme past the register kernels (n + 1 = 243, all 242 clerk
+    results: the workspace reveal of packed_wide.hip) == the step-wise oracle flow."""
+    from tests.test_gpu_parity import wide_schemes
+    ss = next(s for s in wide_schemes() if s.secret_count == 5)
+    m = ss.prime_modulus
+    rng = np.random.default_rng(12)
+    D = 5 * 41 + 2
+    inputs = [rng.integers(0, 1000, size=D) for _ in range(3)]
+    ms = S.ChaChaMasking(m, D, 128)
+    tr = run_aggregation(OracleBackend(), ms, ss, m, D, inputs, Draws(0x5DB))
+    assert tr.positive.tolist() == list(np.sum(inputs, axis=0) % m)
+    for order in (list(range(ss.share_count)), list(range(ss.share_count))[::-2]):
+        indexed = [(c, tr.clerk_results[c]) for c in order]
+        got = engine.recipient_reveal(ms, tr.masks, ss, D, indexed, m)
+        be = OracleBackend()
+        mo = be.secret_reconstruct(ss, D, indexed)
+        exp = be.positive(m, be.secret_unmask(ms, (be.mask_combine(ms, tr.masks), mo)))
+        assert_same(got, exp, "wide")
