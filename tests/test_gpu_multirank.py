@@ -1,6 +1,6 @@
-"""GPU: the multi-GPU helpers (sda_amd.distributed) at world size 2 on the HIP engine.
+"""GPU: the multi-GPU helpers (sda_amd.distributed) at world size 2 and 4 on the HIP engine.
 
-Two child processes (tests/multirank_worker.py, RANK 0 and 1) share cuda:0 and a gloo process group:
+Child processes (tests/multirank_worker.py, one per RANK) share cuda:0 and a gloo process group:
 each runs the engine's device kernels on its own participations / seeds / column slice, and the
 product functions do the exchange (int64 all-reduce + device finalize, or all-gather) on device
 tensors -- the code path of `bench.py --gpus N`, with gloo standing in for RCCL (RCCL refuses two
@@ -32,15 +32,16 @@ def _free_port():
     return port
 
 
-@pytest.fixture(scope="module")
-def results(tmp_path_factory):
+@pytest.fixture(scope="module", params=[2, 4], ids=["world2", "world4"])
+def results(request, tmp_path_factory):
+    world = request.param
     out = str(tmp_path_factory.mktemp("mr") / "res.npz")
-    env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+    env = dict(os.environ, WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                SDA_MR_OUT=out, PYTHONUNBUFFERED="1")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "multirank_worker.py")],
                               env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
-             for r in range(2)]
+             for r in range(world)]
     logs = []
     for p in procs:
         try:
@@ -56,7 +57,7 @@ def results(tmp_path_factory):
 
 
 @pytest.mark.parametrize("N,D", W.CASES)
-def test_world2_rows_and_tiles_equal_single_pass(results, oracle, N, D):
+def test_sharded_rows_and_tiles_equal_single_pass(results, oracle, N, D):
     """combine_rows_sharded / combine_tiles_sharded: participation split, one int64 all-reduce,
     device `% m` == the single sequential pass over all N rows."""
     full = synth.fill(N, D, 0x5DA + 21, 0, W.MOD)
@@ -65,13 +66,13 @@ def test_world2_rows_and_tiles_equal_single_pass(results, oracle, N, D):
     assert np.array_equal(results[f"tiles_{N}x{D}"], exp)
 
 
-def test_world2_mask_combine_seed_split(results, oracle):
+def test_sharded_mask_combine_seed_split(results, oracle):
     """mask_combine_sharded: the recipient's ChaCha mask combine over seeds split across ranks."""
     exp = oracle.chacha_mask_combine(W.MOD, 70_001, W.SEEDS)
     assert np.array_equal(results["mask"], exp)
 
 
-def test_world2_signed_column_split(results, oracle):
+def test_sharded_signed_column_split(results, oracle):
     """combine_columns_sharded: signed shares (order-dependent exact result), column split +
     all-gather, bit-exact with the sequential recurrence."""
     N, D = W.SIGNED

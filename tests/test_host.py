@@ -47,11 +47,11 @@ def _free_port():
     return p
 
 
-def _run_world2(target):
+def _run_world2(target, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=180)
@@ -85,10 +85,11 @@ def _worker_rows(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_sharded_combine_matches_single_pass():
-    """combine_rows_sharded and combine_tiles_sharded at world size 2 (gloo) equal the reference's
-    single sequential pass (combiner.rs:16-28) for non-negative inputs."""
-    res = _run_world2(_worker_rows)
+@pytest.mark.parametrize("world", [2, 8])
+def test_gloo_sharded_combine_matches_single_pass(world):
+    """combine_rows_sharded and combine_tiles_sharded at world size 2 and 8 (gloo; 8 = the driver's
+    node) equal the reference's single sequential pass (combiner.rs:16-28) for non-negative inputs."""
+    res = _run_world2(_worker_rows, world)
     assert res["rows"][0] == res["rows"][1]
     assert res["tiles"][0] == res["tiles"][1]
     assert res["calls"] == ["combine_accumulate_dev", "combine_dev", "combine_finalize_dev"]
@@ -118,10 +119,11 @@ def _worker_mask_columns(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_mask_reduce_and_column_split():
+@pytest.mark.parametrize("world", [2, 8])
+def test_gloo_mask_reduce_and_column_split(world):
     """sda_amd.distributed: ChaCha mask combine split over seeds + reduce, and the signed combine
-    split over columns + all-gather, equal the single-pass reference (gloo, world 2)."""
-    res = _run_world2(_worker_mask_columns)
+    split over columns + all-gather, equal the single-pass reference (gloo, world 2 and 8)."""
+    res = _run_world2(_worker_mask_columns, world)
     for k, (got, exp) in res.items():
         assert got == exp, k
 
