@@ -41,9 +41,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, choices=[1, 3], default=1,
+    ap.add_argument("--config", type=int, choices=[1, 3, 4], default=1,
                     help="1: configs[1] (10k x 1M per GPU, weak scaling); 3: configs[3] (100k x 10M in total, "
-                         "split over the GPUs, streamed through a resident 1000-row tile)")
+                         "split over the GPUs, streamed through a resident 1000-row tile); 4: configs[4]'s "
+                         "recipient (100k ChaCha seeds x 10M-dim mask combine split over the GPUs + packed "
+                         "reveal, unmask, positive)")
+    ap.add_argument("--seeds", type=int, default=100_000, help="configs[4]: participant seeds in total")
     ap.add_argument("--rows", type=int, default=10_000, help="participations per GPU (configs[1]: 10k)")
     ap.add_argument("--dim", type=int, default=1_000_000, help="vector dimension (configs[1]: 1M)")
     ap.add_argument("--shamir-vectors", type=int, default=64, help="participant vectors per share-gen launch")
@@ -198,6 +201,12 @@ def main():
     def barrier():
         if world > 1:
             dist.barrier()
+
+    if args.config == 4:
+        run_config4(args, torch, dist, eng, dev, stream, barrier, world, rank, backend)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     # ---------------- workload: configs[1] (or configs[3]), HBM-resident ----------------
     N, D, m = args.rows, args.dim, MODULUS
@@ -568,7 +577,121 @@ def main():
         dist.destroy_process_group()
 
 
-def valu_roofline(key, ms, waves):
+def run_config4(args, torch, dist, eng, dev, stream, barrier, world, rank, backend):
+    """BASELINE.json configs[4] from the recipient's side (receive.rs:80-157): 100k participants'
+    128-bit ChaCha seeds expanded and combined over a 10M-dim vector (chacha.rs:57-76), the seeds split
+    over the ranks with one int64 all-reduce + device finalize (sda_amd.distributed.mask_combine_sharded),
+    then the packed reveal (k = 8, n = 26, t = 7, 15 clerks, exact) + unmask + positive() of each rank's
+    slice of the batches (sda_recipient_reveal_dev with the combined mask as a Full mask row).  Step = all
+    of it; value = mask elements expanded per second by all ranks."""
+    from sda_amd import distributed as Dd, schemes as S
+    from sda_amd import engine as E
+    sch = S.CONFIG_PACKED
+    p, k, t, n = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count
+    D, total = 10_000_000, args.seeds
+    B = D // k
+    s0, cnt = Dd.shard_range(total, rank, world)
+    allseeds = torch.randint(0, 2**31 - 1, (total, 4), dtype=torch.int32, device=dev,
+                             generator=torch.Generator(device=dev).manual_seed(SEED_BASE + 5))
+    seeds = allseeds[s0:s0 + cnt].contiguous()
+    del allseeds
+    partial = torch.empty(D, dtype=torch.int64, device=dev)
+    mask = torch.empty(D, dtype=torch.int64, device=dev)
+    # this rank's slice of the batches, and its clerks' shares of (secret + mask) mod p
+    b0, nb = Dd.shard_range(B, rank, world)
+    Dl = nb * k
+    sec = torch.empty(Dl, dtype=torch.int64, device=dev)
+    eng.synth_fill_dev(sec.data_ptr(), 1, Dl, SEED_BASE + 4, 0, p, stream())
+    kt = Timer(torch)
+    teng = TimedMask(eng, kt)
+    Dd.mask_combine_sharded(teng, p, D, seeds, partial, mask)            # untimed: the shares' mask
+    masked = torch.remainder(sec + mask[b0 * k:b0 * k + Dl], p)
+    drw = torch.empty((nb, t), dtype=torch.int64, device=dev)
+    eng.synth_fill_dev(drw.data_ptr(), nb, t, SEED_BASE + 44, 0, p - 1, stream())
+    sh = torch.empty((n, nb), dtype=torch.int64, device=dev)
+    eng.packed_generate_dev(sch, masked.data_ptr(), Dl, 1, drw.data_ptr(), sh.data_ptr(), stream())
+    idx = list(range(n - (t + k), n))
+    sub = sh[idx].contiguous()
+    del masked, drw, sh
+    out = torch.empty(Dl, dtype=torch.int64, device=dev)
+    full = S.FullMasking(p)
+    rt = Timer(torch)
+
+    def step(timed):
+        teng.timing = timed
+        Dd.mask_combine_sharded(teng, p, D, seeds, partial, mask)
+        f = lambda: eng.recipient_reveal_dev(full, mask[b0 * k:].data_ptr(), 1, Dl, sch, Dl, idx,  # noqa: E731
+                                             sub.data_ptr(), nb, p, out.data_ptr(), Dl, E.REVEAL_EXACT, stream())
+        rt.record(f) if timed else f()
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ok = torch.equal(out, sec)                 # positive(unmask(reveal)) == the secrets, every element
+    if world > 1:
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+    if not ok:
+        raise SystemExit("configs[4] recipient round trip FAILED")
+    mc_ms, rv_ms = kt.mean_ms(), rt.mean_ms()
+    draws = float(total) * D
+    log(f"[config4] rank {rank}: {args.steps} steps in {dt * 1e3:.1f} ms, mask combine {mc_ms:.2f} ms "
+        f"({cnt} seeds), reveal {rv_ms:.3f} ms ({nb} batches)")
+    if rank != 0:
+        return
+    rec = {
+        "metric": "configs[4] recipient: ChaCha mask elements/s (seeds x 10M-dim mask combine + packed reveal)",
+        "value": round(draws * args.steps / dt, 1), "unit": "mask elements/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic: device-generated 128-bit seeds and secrets (no datasets)",
+        "config": {"workload": "BASELINE.json configs[4], recipient side: ChaCha(128-bit) mask combine of "
+                               f"{total:,} seeds x {D:,}-dim + PackedShamir k=8 n=26 t=7 exact reveal from 15 "
+                               "clerks + unmask + positive",
+                   "seeds_per_gpu": cnt, "dim": D, "modulus": p,
+                   "parallelism": f"seed split x{world}" + ((", RCCL int64 all-reduce" if backend == "nccl" else
+                                                             f", {backend} int64 all-reduce (rehearsal)")
+                                                            if world > 1 else "") + ", batch split reveal"},
+        "mask_combine_kernel_ms": round(mc_ms, 3), "reveal_ms": round(rv_ms, 3),
+        "chacha_blocks_per_s_per_gpu": cnt * D / 8 / (mc_ms * 1e-3),
+        "check": "recipient output == the secrets on every element (all ranks)",
+    }
+    r = valu_roofline("chacha_combine", mc_ms, None, blocks=cnt * D / 8)
+    if r:
+        rec["roofline"] = r
+    print(json.dumps(rec), flush=True)
+
+
+class TimedMask:
+    """HIP events around the ChaCha mask-combine launches of sda_amd.distributed.mask_combine_sharded."""
+
+    def __init__(self, eng, timer):
+        self.eng, self.timer = eng, timer
+        self.timing = False
+
+    def __getattr__(self, name):
+        return getattr(self.eng, name)
+
+    def chacha_mask_combine_dev(self, *a):
+        if self.timing:
+            self.timer.record(lambda: self.eng.chacha_mask_combine_dev(*a))
+        else:
+            self.eng.chacha_mask_combine_dev(*a)
+
+
+def valu_roofline(key, ms, waves, blocks=None):
     """VALU issue roofline of an integer kernel (scripts/valu_mix.py -> profiles/valu_roofline.json):
     lane-ops per launch = SQ_INSTS_VALU (PMC, at this configuration) x 64, or the static VALU count of
     the straight-line kernel x its waves; achieved = lane-ops / live kernel time; peak = the kernel's
@@ -578,7 +701,11 @@ def valu_roofline(key, ms, waves):
             k = json.load(f)["kernels"][key]
     except (OSError, ValueError, KeyError):
         return None
-    if k.get("pmc_valu_insts_per_launch") and (waves is None or k.get("pmc_waves") == waves):
+    if blocks is not None and k.get("pmc_valu_insts_per_launch") and k.get("pmc_blocks"):
+        # another launch size of the same kernel: the PMC instruction count per ChaCha block, scaled
+        insts = k["pmc_valu_insts_per_launch"] / k["pmc_blocks"] * blocks
+        src = "PMC SQ_INSTS_VALU per block (256 x 1M launch) x blocks"
+    elif blocks is None and k.get("pmc_valu_insts_per_launch") and (waves is None or k.get("pmc_waves") == waves):
         insts, src = k["pmc_valu_insts_per_launch"], "PMC SQ_INSTS_VALU"
     elif waves is not None:
         insts, src = k["static_valu"] * waves, "static VALU count x waves"

@@ -42,6 +42,9 @@ PMC_NAMES = {
     "chacha_combine": "chacha_combine_kernel<true, false>",
 }
 
+# ChaCha20 blocks of the counted launch (bench.py's chacha leg: 256 seeds x 1M-dim, 8 draws per block)
+PMC_BLOCKS = {"chacha_combine": 256 * 1_000_000 // 8}
+
 # instruction class -> the ubench_int row(s) that measured it
 CLASSES = [
     (r"^v_(add|sub|subrev)_u32$", ["v_add_u32", "v_sub_u32"]),
@@ -133,6 +136,8 @@ def main():
             rec["pmc_valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
             rec["pmc_waves"] = c.get("SQ_WAVES")
             rec["pmc_source"] = sources[hit]
+            if key in PMC_BLOCKS:      # work units of the counted launch, to scale to other launch sizes
+                rec["pmc_blocks"] = PMC_BLOCKS[key]
         out["kernels"][key] = rec
     json.dump(out, sys.stdout, indent=1)
 
