@@ -299,6 +299,99 @@ __global__ __launch_bounds__(64) void packed_reveal_fixup_kernel(const int64_t* 
     }
 }
 
+// The same fix-up with one WAVE per logged batch (m <= 64 points): lane i holds Newton point i, so each
+// of the m - 1 levels of tss' divided differences is one parallel step (lane i needs only lane i - 1's
+// value of the previous level -- the in-place descending loop reads exactly that), and lane e < k folds
+// newton_evaluate at omega_secrets^(e+1) with the coefficients broadcast from their lanes.  Exact i64
+// arithmetic with truncated `%` throughout (the generic path's), so in-range and raw i64 shares are
+// handled alike.  A trapped batch is a serial latency chain for one lane on the register path (~40 us);
+// spread over the wave it is m + k short steps.
+// Rust `v % p` for |v| < 2^62 (a product of two values in (-p, p), p < 2^31): the quotient from a double
+// product (exact operands, relative error 2^-53, so |q - v/p| < 1) and one signed correction step.
+__device__ __forceinline__ int64_t trem_prod(int32_t a, int32_t b, uint32_t p, double pinv) {
+    const int64_t v = (int64_t)a * b;
+    const int64_t q = (int64_t)__builtin_trunc((double)a * (double)b * pinv);
+    int64_t r = v - q * (int64_t)p;                     // v - trunc(v/p) p, off by at most one p
+    if (v >= 0) { r = r < 0 ? r + p : r; r = r >= (int64_t)p ? r - p : r; }
+    else { r = r > 0 ? r - p : r; r = r <= -(int64_t)p ? r + p : r; }
+    return r;
+}
+// Rust `v % p` for |v| < 2p.
+__device__ __forceinline__ int32_t trem_small(int64_t v, uint32_t p) {
+    const int64_t P = p;
+    return (int32_t)(v >= P ? v - P : (v <= -P ? v + P : v));
+}
+
+// The same fix-up with one WAVE per logged batch (m <= 64 points): lane i holds Newton point i, so each
+// of the m - 1 levels of tss' divided differences is one parallel step (lane i needs only lane i - 1's
+// value of the previous level -- the in-place descending loop reads exactly that), and lane e < k folds
+// newton_evaluate at omega_secrets^(e+1) with the coefficients broadcast from their lanes.  Each lane
+// preloads its column of the inverse table and its row of Newton bases, so no step waits on memory.
+// Shares in (-p, p) keep every tss intermediate in (-p, p): 32-bit values, `%` of products through
+// trem_prod; otherwise (raw i64 shares) the generic i64 arithmetic.  A trapped batch is a serial
+// latency chain for one lane on the register path (~40 us); spread over the wave it is m + k short steps.
+template <int MMAX>
+__global__ __launch_bounds__(64) void packed_reveal_fixup_wave_kernel(const int64_t* __restrict__ shares, uint64_t B,
+                                                                      uint64_t D, uint64_t n_vec,
+                                                                      int64_t* __restrict__ out, uint32_t n_idx,
+                                                                      uint32_t k, const uint32_t* __restrict__ tab,
+                                                                      uint32_t p, const unsigned int* __restrict__ log) {
+    static_assert(MMAX <= 64, "one lane per Newton point");
+    const uint32_t n = *log;
+    if (n == 0) return;
+    const bool all = n > kGenLogCap;
+    const uint64_t total = all ? B * n_vec : (uint64_t)n;
+    if ((uint64_t)blockIdx.x >= total) return;          // waves without a batch skip the table preload
+    const uint64_t* list = reinterpret_cast<const uint64_t*>(log + 16);
+    const uint32_t m = n_idx + 1, lane = threadIdx.x;
+    const Mod64 P = make_mod64((int64_t)p);
+    const double pinv = 1.0 / (double)p;
+    int32_t inv[MMAX], np[MMAX];          // this lane's inv[j][lane] and np[lane][i]
+#pragma unroll
+    for (int j = 0; j < MMAX; ++j) {
+        inv[j] = (j >= 1 && lane < MMAX) ? (int32_t)tab[OFF_INV + j * TS + (lane < MMAX ? lane : 0)] : 0;
+        np[j] = lane < k ? (int32_t)tab[OFF_NP + (lane < k ? lane : 0) * TS + j] : 0;
+    }
+    for (uint64_t w = blockIdx.x; w < total; w += gridDim.x) {
+        const uint64_t gb = all ? w : list[w];
+        const uint64_t vec = gb / B, b = gb - vec * B;
+        // point 0 is the inserted (1, 0); point i >= 1 is clerk share i - 1 (batched.rs:83-85)
+        int64_t s = (lane >= 1 && lane < m) ? shares[vec * (uint64_t)n_idx * B + (uint64_t)(lane - 1) * B + b] : 0;
+        const bool small = __all((uint64_t)(s + (int64_t)p - 1) < (uint64_t)(2 * (int64_t)p - 1));
+        const uint32_t lim = b * k < D ? (uint32_t)(D - b * k < k ? D - b * k : k) : 0u;
+        int64_t acc = 0;
+        if (small) {
+            int32_t x = (int32_t)s;
+#pragma unroll
+            for (int j = 1; j < MMAX; ++j) {
+                const int32_t prev = __shfl_up(x, 1);
+                if ((uint32_t)j < m && lane >= (uint32_t)j && lane < m)
+                    x = (int32_t)trem_prod(trem_small((int64_t)x - prev, p), inv[j], p, pinv);
+            }
+            int32_t a = 0;
+#pragma unroll
+            for (int i = 0; i < MMAX; ++i) {
+                const int32_t c = __shfl(x, i);
+                if ((uint32_t)i < m) a = trem_small((int64_t)a + trem_prod(c, np[i], p, pinv), p);
+            }
+            acc = a;
+        } else {
+#pragma unroll
+            for (int j = 1; j < MMAX; ++j) {
+                const int64_t prev = __shfl_up(s, 1);
+                if ((uint32_t)j < m && lane >= (uint32_t)j && lane < m)
+                    s = trem64(wmul(trem64(wsub(s, prev), P), inv[j]), P);
+            }
+#pragma unroll
+            for (int i = 0; i < MMAX; ++i) {
+                const int64_t c = __shfl(s, i);
+                if ((uint32_t)i < m) acc = trem64(wadd(acc, trem64(wmul(c, np[i]), P)), P);
+            }
+        }
+        if (lane < lim) out[vec * D + b * k + lane] = acc;                     // batched.rs:94
+    }
+}
+
 template <int NMAX, bool STAGED>
 __global__ __launch_bounds__(256) void packed_reveal_canon_kernel(const int64_t* __restrict__ shares, uint64_t B,
                                                                   uint64_t D, int64_t* __restrict__ out,
@@ -384,10 +477,14 @@ hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        if (MM <= 16 && k <= 8)
-            hipLaunchKernelGGL((packed_reveal_fixup_kernel<MM, MM <= 16 ? 8 : 0>), dim3(64), dim3(64), 0, s, a.shares,
-                               B, a.dimension, a.n_vectors, a.out, n_idx, k, tab, M, log);
-        else
+        if constexpr (MM <= 64) {
+            if (k <= 64)
+                hipLaunchKernelGGL((packed_reveal_fixup_wave_kernel<MM>), dim3(1024), dim3(64), 0, s, a.shares, B,
+                                   a.dimension, a.n_vectors, a.out, n_idx, k, tab, M.p, log);
+            else
+                hipLaunchKernelGGL((packed_reveal_fixup_kernel<MM, 0>), dim3(64), dim3(64), 0, s, a.shares, B,
+                                   a.dimension, a.n_vectors, a.out, n_idx, k, tab, M, log);
+        } else
             hipLaunchKernelGGL((packed_reveal_fixup_kernel<MM, 0>), dim3(64), dim3(64), 0, s, a.shares, B,
                                a.dimension, a.n_vectors, a.out, n_idx, k, tab, M, log);
     } else {

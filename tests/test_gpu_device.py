@@ -179,3 +179,22 @@ def test_distributed_helpers_single_rank(engine, oracle):
     Dd.combine_columns_sharded(engine, m, xd, out)
     torch.cuda.synchronize()
     assert_same(out.cpu().numpy(), oracle.combine(m, x))
+
+
+def test_packed_reveal_fixup_overflow(engine, oracle):
+    """More out-of-range (raw i64) share batches than the reveal's fix-up log holds: every batch is
+    recomputed exactly by the fix-up kernel (one wave per batch)."""
+    sch = S.CONFIG_PACKED
+    p, k, t, n = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count
+    B = 70_001                                  # > kGenLogCap (65536) logged batches
+    D = B * k
+    rng = np.random.default_rng(0x5DB)
+    idx = list(range(3, 3 + t + k))
+    raw = rng.integers(-(2**40), 2**40, size=(len(idx), B), dtype=np.int64)
+    got = engine.secret_reconstruct(sch, D, [(c, raw[j]) for j, c in enumerate(idx)])
+    pp = oracle.packed_params(k, n, t, p, sch.omega_secrets, sch.omega_shares)
+    sample = sorted(set(int(b) for b in np.random.default_rng(4).integers(0, B, 40)) | {0, B - 1})
+    rc, exp = oracle.packed_reconstruct(pp, k * len(sample), idx, raw[:, sample])
+    assert rc == 0
+    for j, b in enumerate(sample):
+        assert_same(got[b * k:(b + 1) * k], exp[j * k:(j + 1) * k])
