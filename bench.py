@@ -423,6 +423,16 @@ def main():
         for i in range(4):
             f = lambda: eng.clerk_decode_combine_dev(m, buf.data_ptr(), off, cout.data_ptr(), Dc, stream())  # noqa
             ct.record(f) if i else f()
+        # the decode-to-int32-matrix + combine path the fused one replaced (same call, SDA_CODEC_PATH knob)
+        mt = Timer(torch)
+        cout_m = torch.empty(Dc, dtype=torch.int64, device=dev)
+        os.environ["SDA_CODEC_PATH"] = "matrix"
+        try:
+            for i in range(4):
+                f = lambda: eng.clerk_decode_combine_dev(m, buf.data_ptr(), off, cout_m.data_ptr(), Dc, stream())  # noqa
+                mt.record(f) if i else f()
+        finally:
+            del os.environ["SDA_CODEC_PATH"]
         torch.cuda.synchronize()
         if not args.no_check:
             if not torch.equal(mat, x):
@@ -433,7 +443,9 @@ def main():
             if not (torch.equal(torch.remainder(r, m), torch.remainder(x[:, cols].sum(0), m))
                     and bool((r.abs() < m).all())):
                 raise SystemExit("codec decode+combine FAILED")
-        e_ms, d_ms, c_ms = et.mean_ms(), dt_.mean_ms(), ct.mean_ms()
+            if not torch.equal(cout, cout_m):
+                raise SystemExit("codec fused vs matrix decode+combine FAILED")
+        e_ms, d_ms, c_ms, cm_ms = et.mean_ms(), dt_.mean_ms(), ct.mean_ms(), mt.mean_ms()
         side["codec"] = {
             "config": f"varint payloads of {Nc} participations x 1M-dim signed field shares "
                       f"({payload / Nc / Dc:.2f} B/share)",
@@ -441,6 +453,9 @@ def main():
             "decode_ms": d_ms, "decode_payload_GBps": payload / (d_ms * 1e-3) / 1e9,
             "decode_hbm_GBps": (payload + 8.0 * Nc * Dc) / (d_ms * 1e-3) / 1e9,
             "decode_combine_ms": c_ms, "decode_combine_shares_per_s": Nc * Dc / (c_ms * 1e-3),
+            "decode_combine_payload_GBps": payload / (c_ms * 1e-3) / 1e9,
+            "decode_combine_path": "fused (count pass + one column-tile decode+combine pass)",
+            "decode_combine_matrix_ms": cm_ms,
             "encode_ms": e_ms, "encode_hbm_GBps": (payload + 8.0 * Nc * Dc) / (e_ms * 1e-3) / 1e9,
         }
         log(f"[codec] {json.dumps(side['codec'])}")

@@ -19,6 +19,15 @@
 //           start is the previous terminator, within the 16-byte halo) into out[blob][index].
 // Irregular blobs (malformed streams) are decoded by a sequential exact kernel instead.
 // Roofline: HBM.  Algorithmic bytes = payload bytes read + 8 B per decoded element written.
+//
+// The clerk's decode -> combine (clerk.rs:79-86) fuses pass C with the combine instead of writing a
+// [N][len] matrix: pass A also counts the terminators of every 256-byte sub-chunk; a plan kernel
+// locates, per (column tile of kDcTile elements, blob), the sub-chunk holding the terminator that ends
+// the previous tile and how many of its terminators precede the tile; then one workgroup per column
+// tile walks the blobs in order, decodes its tile's slice of each payload (read once, plus at most a
+// sub-chunk per tile edge) and folds it into combiner.rs:16-28's exact recurrence in registers.
+#include <stdlib.h>
+
 #include "kernels.h"
 
 namespace sda {
@@ -41,6 +50,15 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return x;
+}
+
+// Sum over each row of 16 lanes, in the row's last lane (the first four steps of wave_incl_scan).
+__device__ __forceinline__ uint32_t row16_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
     return x;
 }
 
@@ -113,12 +131,17 @@ __device__ __forceinline__ bool region_of(const uint64_t* __restrict__ blob_regi
     return true;
 }
 
-// pass A: terminator count of each region; irregular-blob flag.
+// pass A: terminator count of each region; irregular-blob flag.  With sub_count (the clerk's fused
+// decode -> combine) also the count of every 256-byte sub-chunk (16 words = one row of 16 lanes):
+// sub_count[region * 64 + sub-chunk].
+constexpr uint32_t kSubChunk = 256;
+constexpr uint32_t kSubPerRegion = (uint32_t)(kRegionBytes / kSubChunk);
 __global__ __launch_bounds__(kThreads) void varint_count_kernel(const uint8_t* __restrict__ bytes,
                                                                 const uint64_t* __restrict__ blob_region,
                                                                 const uint64_t* __restrict__ blob_off, uint32_t y0,
                                                                 uint32_t* __restrict__ region_count,
-                                                                uint32_t* __restrict__ blob_irregular) {
+                                                                uint32_t* __restrict__ blob_irregular,
+                                                                uint16_t* __restrict__ sub_count) {
     uint32_t b;
     uint64_t r, word;
     if (!region_of(blob_region, blob_off, y0, &b, &r, &word)) return;
@@ -144,19 +167,30 @@ __global__ __launch_bounds__(kThreads) void varint_count_kernel(const uint8_t* _
     }
     if (threadIdx.x == 0) cm_l[0] = make_window(make_uint4(0, 0, 0, 0), halo, word - 1, begin, end).cont >> 16;
     __syncthreads();
-    uint32_t n = 0, bad = 0;
+    uint32_t n = 0, bad = 0, lng = 0;
 #pragma unroll
     for (int k = 0; k < kWPT; ++k) {
         const uint32_t wl = threadIdx.x + k * kThreads;
-        n += __builtin_popcount(W[k].term & W[k].valid);
+        const uint32_t nk = __builtin_popcount(W[k].term & W[k].valid);
+        n += nk;
+        if (sub_count) {
+            const uint32_t rs = row16_incl_scan(nk);
+            if ((threadIdx.x & 15) == 15) sub_count[r * kSubPerRegion + (wl >> 4)] = (uint16_t)rs;
+        }
         // 11 continuation bytes in a row ending inside this word?
         const uint32_t cont = W[k].cont | cm_l[wl];
-        uint32_t run = cont;
+        uint32_t run = cont, run5 = 0;
 #pragma unroll
-        for (int q = 1; q <= 10; ++q) run &= cont << q;
+        for (int q = 1; q <= 10; ++q) {
+            run &= cont << q;
+            if (q == 4) run5 = run;                      // 5 continuation bytes: an element of >= 6 bytes
+        }
         bad |= run & W[k].valid;
+        lng |= run5 & W[k].valid;
     }
-    if (bad) atomicOr(&blob_irregular[b], 1u);
+    // bit 0: irregular (sequential decoder); bit 1: an element of >= 6 bytes (the fused decode -> combine
+    // then takes its multi-round variant)
+    if (bad || lng) atomicOr(&blob_irregular[b], (bad ? 1u : 0u) | (lng ? 2u : 0u));
     // block reduction (one value per region)
     __shared__ uint32_t red[kThreads / 64];
     for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o);
@@ -207,6 +241,37 @@ __device__ __forceinline__ uint64_t leb_pack8(uint64_t x) {
     return x;
 }
 
+// The element of `len` bytes (1..11, a regular blob) that starts at byte P of the LDS image lb (read
+// as funnel-shifted dwords; lb holds at least 12 readable bytes past P): zigzag + LEB128 -> i64.
+__device__ __forceinline__ int64_t varint_value_at(const uint32_t* lb, uint32_t P, uint32_t len) {
+    const uint32_t q = P >> 2, sh = (P & 3) * 8;
+    const uint32_t d0 = lb[q], d1 = lb[q + 1], d2 = lb[q + 2];
+    const uint32_t b0 = __builtin_amdgcn_alignbit(d1, d0, sh), b1 = __builtin_amdgcn_alignbit(d2, d1, sh);
+    int64_t val;
+    if (len <= 5) {
+        // bytes 0..3 (masked to the element) -> 4 x 7-bit groups: two bit-field merges
+        const uint32_t l4 = len < 4 ? len : 4u, cut = 32 - 8 * l4;
+        uint32_t x = ((b0 << cut) >> cut) & 0x7F7F7F7Fu;
+        x = (x & 0x007F007Fu) | ((x >> 1) & ~0x007F007Fu);  // byte pairs -> 14-bit lanes (bit 15 junk)
+        x = (x & 0x00003FFFu) | ((x >> 2) & ~0x00003FFFu);  // -> 28 bits (bits 28..31 clear)
+        const uint32_t g4 = len == 5 ? (b1 & 0x7Fu) : 0u;   // group 4 at bit 28
+        const uint32_t zl = x | (g4 << 28), zh = g4 >> 4;
+        val = (int64_t)((((uint64_t)zh << 32) | zl) >> 1) ^ -(int64_t)(zl & 1u);
+    } else {
+        const uint32_t b2 = __builtin_amdgcn_alignbit(lb[q + 3], d2, sh);
+        uint64_t lo = ((uint64_t)b1 << 32) | b0;
+        if (len < 8) lo &= (1ull << (8 * len)) - 1;
+        uint64_t z = leb_pack8(lo);
+        if (len > 8) {          // groups 8, 9, 10 at shifts 56, 63, 70 & 63 = 6 (Rust release)
+            const uint32_t hb = b2 & ((len >= 11) ? 0xFFFFFFu : (len == 10 ? 0xFFFFu : 0xFFu));
+            z |= ((uint64_t)(hb & 0x7F) << 56) | ((uint64_t)((hb >> 8) & 0x7F) << 63) |
+                 ((uint64_t)((hb >> 16) & 0x7F) << 6);
+        }
+        val = (int64_t)((z >> 1) ^ (0 - (z & 1)));
+    }
+    return val;
+}
+
 // pass C: decode.  The region's bytes (plus a 16-byte halo on each side) are staged in LDS, with
 // each word's 16-bit continuation mask beside them (so a window's previous-word mask is one LDS
 // read).  The region is walked as kWPT sub-regions of one word per thread.  Per sub-region a
@@ -228,7 +293,7 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
                                                                  uint32_t* __restrict__ wide) {
     uint32_t b;
     uint64_t r, word;
-    if (!region_of(blob_region, blob_off, y0, &b, &r, &word) || blob_irregular[b]) return;
+    if (!region_of(blob_region, blob_off, y0, &b, &r, &word) || (blob_irregular[b] & 1u)) return;
     __shared__ uint32_t lb[(kRegionBytes + 32) / 4];          // [halo 16 B | region 16 KiB | tail 16 B]
     __shared__ uint32_t cml[kWPT * kThreads + 1];             // continuation mask of lb word w at [w]
     __shared__ uint32_t wsum[kThreads / 64];
@@ -301,10 +366,10 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
         for (uint32_t i = threadIdx.x; i < total; i += kThreads) {
             const uint32_t P = el[i] & 0xFFFFu;                  // byte position in lb
             const uint32_t len = el[i] >> 16;                     // 1..11 on regular blobs
-            const uint32_t q = P >> 2, sh = (P & 3) * 8;
-            const uint32_t d0 = lb[q], d1 = lb[q + 1], d2 = lb[q + 2];
-            const uint32_t b0 = __builtin_amdgcn_alignbit(d1, d0, sh), b1 = __builtin_amdgcn_alignbit(d2, d1, sh);
             if constexpr (sizeof(OutT) < 8) {
+                const uint32_t q = P >> 2, sh = (P & 3) * 8;
+                const uint32_t d0 = lb[q], d1 = lb[q + 1], d2 = lb[q + 2];
+                const uint32_t b0 = __builtin_amdgcn_alignbit(d1, d0, sh), b1 = __builtin_amdgcn_alignbit(d2, d1, sh);
                 // int32 output: elements of <= 5 bytes whose zigzag value is below 2^32 (anything
                 // else sets *wide and the caller decodes the job as i64)
                 const uint32_t l4 = len < 4 ? len : 4u, cut = 32 - 8 * l4;
@@ -317,28 +382,7 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
                 dst[base + i] = (OutT)((zl >> 1) ^ (0u - (zl & 1u)));
                 continue;
             }
-            int64_t val;
-            if (len <= 5) {
-                // bytes 0..3 (masked to the element) -> 4 x 7-bit groups: two bit-field merges
-                const uint32_t l4 = len < 4 ? len : 4u, cut = 32 - 8 * l4;
-                uint32_t x = ((b0 << cut) >> cut) & 0x7F7F7F7Fu;
-                x = (x & 0x007F007Fu) | ((x >> 1) & ~0x007F007Fu);  // byte pairs -> 14-bit lanes (bit 15 junk)
-                x = (x & 0x00003FFFu) | ((x >> 2) & ~0x00003FFFu);  // -> 28 bits (bits 28..31 clear)
-                const uint32_t g4 = len == 5 ? (b1 & 0x7Fu) : 0u;   // group 4 at bit 28
-                const uint32_t zl = x | (g4 << 28), zh = g4 >> 4;
-                val = (int64_t)((((uint64_t)zh << 32) | zl) >> 1) ^ -(int64_t)(zl & 1u);
-            } else {
-                const uint32_t b2 = __builtin_amdgcn_alignbit(lb[q + 3], d2, sh);
-                uint64_t lo = ((uint64_t)b1 << 32) | b0;
-                if (len < 8) lo &= (1ull << (8 * len)) - 1;
-                uint64_t z = leb_pack8(lo);
-                if (len > 8) {          // groups 8, 9, 10 at shifts 56, 63, 70 & 63 = 6 (Rust release)
-                    const uint32_t hb = b2 & ((len >= 11) ? 0xFFFFFFu : (len == 10 ? 0xFFFFu : 0xFFu));
-                    z |= ((uint64_t)(hb & 0x7F) << 56) | ((uint64_t)((hb >> 8) & 0x7F) << 63) |
-                         ((uint64_t)((hb >> 16) & 0x7F) << 6);
-                }
-                val = (int64_t)((z >> 1) ^ (0 - (z & 1)));
-            }
+            const int64_t val = varint_value_at(lb, P, len);
             dst[base + i] = (OutT)val;
         }
         base += total;
@@ -348,6 +392,241 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
     }
 }
 
+// ---------------- the clerk's fused decode -> combine ----------------
+// Column tile of the fused decode -> combine: 1,536 columns = 3 per lane of a 512-lane workgroup.  With
+// elements of <= 5 bytes (every field share: |v| < 2^31) a tile's slice of a payload is at most
+// 256 + 5 x 1536 + 256 = 8 KiB = one 16-byte word per lane.
+constexpr uint32_t kDcThreads = 512;
+constexpr uint32_t kDcTile = 3 * kDcThreads;
+
+// Per (column tile t >= 1, blob b): the 256-byte sub-chunk holding the terminator of element t*kDcTile - 1
+// (the previous tile's last element) and the number of the blob's terminators in that sub-chunk up to
+// and including it; tile 0 starts at the blob's first byte.  plan[t * n_blobs + b] = byte << 16 | skip.
+// One thread per (region, blob) (grid.y = blob): it emits the entries of every tile whose boundary
+// element falls in its region, walking the region's 64 sub-chunk counts once (no search).
+__global__ __launch_bounds__(kThreads) void varint_tile_plan_kernel(const uint64_t* __restrict__ blob_off,
+                                                                    const uint64_t* __restrict__ blob_region,
+                                                                    const uint64_t* __restrict__ region_base,
+                                                                    const uint16_t* __restrict__ sub_count,
+                                                                    uint32_t y0, uint64_t n_blobs, uint64_t ntiles,
+                                                                    uint64_t* __restrict__ plan) {
+    const uint64_t b = y0 + blockIdx.y;
+    const uint64_t r0 = blob_region[b], r1 = blob_region[b + 1];
+    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    const uint64_t beg = blob_off[b];
+    if (i == 0) plan[b] = (beg & ~(uint64_t)15) << 16;              // tile 0
+    if (r0 + i >= r1) return;
+    const uint64_t r = r0 + i;
+    const uint64_t E0 = region_base[r];
+    const uint64_t E1 = r + 1 < r1 ? region_base[r + 1] : ~(uint64_t)0;   // last region: to the blob's end
+    // tiles t >= 1 whose boundary element t*T - 1 lies in [E0, E1)
+    uint64_t t = E0 / kDcTile + 1;
+    if (t >= ntiles || t * kDcTile - 1 >= E1) return;
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    const u32x4_t* sc4 = reinterpret_cast<const u32x4_t*>(sub_count + r * kSubPerRegion);
+    u32x4_t w[kSubPerRegion / 8];
+    static_for<0, kSubPerRegion / 8>([&](auto j) { w[j] = sc4[j]; });
+    const uint64_t rbyte = (beg / kRegionBytes + i) * kRegionBytes;
+    uint64_t E = E0, e = t * kDcTile - 1;
+    static_for<0, kSubPerRegion>([&](auto s) {
+        const uint32_t c = (w[s / 8][(s % 8) / 2] >> (16 * (s % 2))) & 0xFFFFu;
+        while (e < E + c && e < E1 && t < ntiles) {                 // boundary e in sub-chunk s
+            plan[t * n_blobs + b] = ((rbyte + (uint64_t)s * kSubChunk) << 16) | (e - E + 1);
+            ++t;
+            e += kDcTile;
+        }
+        E += c;
+    });
+}
+
+// make_window_cm in 32-bit offsets relative to a slice start: own word at byte w0 (>= 0), the blob at
+// [lo_b, hi_b) (clamped to +-2^30 by the caller).
+__device__ __forceinline__ Window window_rel(uint32_t cm, int32_t w0, int32_t lo_b, int32_t hi_b) {
+    Window W;
+    const int32_t lo = lo_b - (w0 - 16), hi = hi_b - (w0 - 16);
+    const int l = lo < 0 ? 0 : (lo > 32 ? 32 : lo);
+    const int h = hi < 0 ? 0 : (hi > 32 ? 32 : hi);
+    uint32_t in = 0;
+    if (h > l) in = (h - l == 32 ? 0xFFFFFFFFu : ((1u << (h - l)) - 1u)) << l;
+    W.valid = in & 0xFFFF0000u;
+    const uint32_t lastbit = (hi >= 1 && hi <= 32) ? 1u << (hi - 1) : 0u;
+    W.cont = cm & in;
+    W.term = (~cm & in) | (lastbit & in);
+    return W;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_word(const uint8_t* bytes, uint64_t w) {      // read once: non-temporal
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(bytes) + w);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// One workgroup (512 lanes) per column tile [e0, e0 + kDcTile): for every blob in order, its tile slice
+// -- the words from the plan's sub-chunk to the end of the sub-chunk the next tile's plan points at, one
+// per lane -- is staged in LDS, one block scan ranks its terminators, the ones with rank in
+// [skip, skip + tile) are compacted as (start, length), and lane l decodes elements l, l + 512, l + 1024
+// (its own columns) straight into combiner.rs:16-28's recurrence (add_trem: exact for signed shares,
+// reference order).  LDS images are double-buffered by round parity, so a round takes two barriers.
+// MULTI (the job has an element of >= 6 bytes): a slice longer than 512 words takes further rounds, the
+// previous round's last word as the halo; otherwise the body is straight-line, which keeps hipcc's load
+// counters exact.  Each lane's round-0 word is loaded DEPTH blobs ahead (register ring), so DEPTH blobs'
+// loads are in flight while one is decoded.  Regular blobs only (no run of 11 continuation bytes).
+template <int DEPTH, bool MULTI>
+__global__ __launch_bounds__(kDcThreads) __attribute__((amdgpu_waves_per_eu(6, 8)))
+void varint_decode_combine_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ blob_off,
+                                  uint64_t n_blobs, const uint64_t* __restrict__ plan, uint64_t ntiles,
+                                  uint64_t dim, int64_t* __restrict__ out, Mod64 M, bool small_m) {
+    constexpr uint32_t NT = kDcThreads, NW = kDcThreads, TILE = kDcTile, COLS = TILE / NT;
+    __shared__ uint4 lb4[2][NW + 2];                      // [halo word | NW words | zero tail] per parity
+    __shared__ uint32_t cml[2][NW + 1];                   // continuation mask of lb4[.][w] at [w]
+    __shared__ uint32_t wsum[NT / 64];
+    __shared__ uint32_t el[2][TILE];                      // element i of the tile: start | len << 16
+    __shared__ uint4 halo4;                               // the last word of the previous round (MULTI)
+    __shared__ uint32_t halo_cm;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t t = blockIdx.x;
+    const uint64_t e0 = t * TILE;
+    const uint32_t tile = (uint32_t)(dim - e0 < TILE ? dim - e0 : TILE);
+    if (tid < 2) lb4[tid][NW + 1] = make_uint4(0, 0, 0, 0);
+    uint32_t par = 0;                                     // LDS parity of the current round
+
+    // the tile's slice of blob b: words [a / 16, (end + 15) / 16); terminators of rank < skip end the
+    // previous tile's elements
+    struct Slice { uint64_t wa, nw, beg, bend; uint32_t skip; };
+    auto slice = [&](uint64_t b) {
+        Slice S;
+        const uint64_t pe = plan[t * n_blobs + b];
+        S.wa = pe >> 20;
+        S.skip = (uint32_t)(pe & 0xFFFF);
+        S.beg = blob_off[b];
+        S.bend = blob_off[b + 1];
+        uint64_t end = S.bend;
+        if (t + 1 < ntiles) {
+            const uint64_t an = (plan[(t + 1) * n_blobs + b] >> 16) + kSubChunk;
+            end = an < S.bend ? an : S.bend;
+        }
+        S.nw = ((end + 15) >> 4) - S.wa;
+        return S;
+    };
+    // unconditional load (clamped into the slice): a load under a lane branch leaves the wait counter
+    // unknown at the join, and hipcc then drains every load in flight (vmcnt(0)) at the ring's use
+    auto load_word = [&](uint64_t wa, uint64_t nw, uint64_t r0) {
+        const uint64_t w = r0 + tid;
+        return nt_word(bytes, wa + (w < nw ? w : nw - 1));
+    };
+
+    int64_t acc[COLS];
+    static_for<0, COLS>([&](auto c) { acc[c] = 0; });
+
+    // One round over words [r0, r0 + NW) of slice S (v: this lane's word, zero past the slice): stage in
+    // LDS, rank the terminators, compact the tile's elements among them, decode this lane's columns.
+    // `staged()` runs once the word is in LDS (the ring slot it came from may be refilled).  Returns the
+    // round's terminator count.
+    auto round = [&](const Slice& S, int32_t lo_b, int32_t hi_b, uint64_t r0, uint32_t rank, const uint4& v,
+                     auto&& staged) __attribute__((always_inline)) {
+        const uint32_t skip = S.skip;
+        uint4* L4 = lb4[par];
+        uint32_t* CM = cml[par];
+        uint32_t* EL = el[par];
+        const uint32_t cm = cont_mask(v);
+        L4[tid + 1] = v;
+        CM[tid + 1] = cm;
+        const int32_t w0 = (int32_t)((r0 + tid) * 16);
+        const Window Wo = window_rel(cm << 16, w0, lo_b, hi_b);
+        const uint32_t tm = Wo.term & Wo.valid;
+        const uint32_t n = __builtin_popcount(tm);
+        staged();
+        if (tid == 0) {
+            if (!MULTI || r0 == 0) { L4[0] = make_uint4(0, 0, 0, 0); CM[0] = 0; }
+            else { L4[0] = halo4; CM[0] = halo_cm; }
+        }
+        const uint32_t incl = wave_incl_scan(n);
+        if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+        __syncthreads();
+        uint32_t q = rank + incl - n, total = 0;
+        static_for<0, NT / 64>([&](auto w) {
+            const uint32_t x = wsum[w];
+            if ((uint32_t)w < (tid >> 6)) q += x;
+            total += x;
+        });
+        if (tm && q + n > skip && q < skip + tile) {
+            // element starts as in pass C (previous boundary in the 32-byte window)
+            const Window W = window_rel(CM[tid] | (cm << 16), w0, lo_b, hi_b);
+            const uint32_t boundary = W.term | ~(W.term | W.cont);
+            const uint32_t pos0 = tid * 16;
+            uint32_t rem = tm;
+            const uint32_t below = boundary & ((1u << __builtin_ctz(rem)) - 1u);
+            uint32_t st = below ? 32 - __builtin_clz(below) : 0;
+            do {
+                const uint32_t j = __builtin_ctz(rem);
+                rem &= rem - 1;
+                const uint32_t i = q - skip;              // wraps (huge) below skip
+                if (i < tile) EL[i] = (pos0 + st) | ((j - st + 1) << 16);
+                ++q;
+                st = j + 1;
+            } while (rem);
+        }
+        if (MULTI && tid == 0 && r0 + NW < S.nw) { halo4 = L4[NW]; halo_cm = CM[NW]; }
+        __syncthreads();
+        // elements [ilo, ihi) of the tile end in this round; lane l owns columns l + 512 c
+        const uint32_t ilo = rank > skip ? (rank - skip < tile ? rank - skip : tile) : 0u;
+        const uint32_t ihi = rank + total > skip ? (rank + total - skip < tile ? rank + total - skip : tile) : 0u;
+        const uint32_t* lb = reinterpret_cast<const uint32_t*>(L4);
+        static_for<0, COLS>([&](auto c) {
+            const uint32_t i = tid + c * NT;
+            if (i >= ilo && i < ihi) {
+                const uint32_t e = EL[i];
+                acc[c] = add_trem(acc[c], varint_value_at(lb, e & 0xFFFFu, e >> 16), M, small_m);
+            }
+        });
+        par ^= 1u;
+        return total;
+    };
+
+    // blob b: round 0 straight from its ring slot (refilled with blob `next`'s word as soon as it is
+    // staged); further rounds (MULTI) load their words synchronously
+    auto blob = [&](uint64_t b, uint4& slot, bool refill, uint64_t next) __attribute__((always_inline)) {
+        const Slice S = slice(b);
+        auto rel = [&](uint64_t x) {                      // blob bounds in bytes from the slice start
+            const int64_t d = (int64_t)(x - (S.wa << 4));
+            return (int32_t)(d < -(1ll << 30) ? -(1ll << 30) : (d > (1ll << 30) ? (1ll << 30) : d));
+        };
+        const int32_t lo_b = rel(S.beg), hi_b = rel(S.bend);
+        const uint4 v = tid < S.nw ? slot : make_uint4(0, 0, 0, 0);
+        uint32_t rank = round(S, lo_b, hi_b, 0, 0, v, [&] {
+            if (refill) { const Slice N = slice(next); slot = load_word(N.wa, N.nw, 0); }
+        });
+        if constexpr (MULTI) {
+            for (uint64_t r0 = NW; r0 < S.nw && rank < S.skip + tile; r0 += NW) {
+                const uint4 w = load_word(S.wa, S.nw, r0);
+                rank += round(S, lo_b, hi_b, r0, rank, r0 + tid < S.nw ? w : make_uint4(0, 0, 0, 0), [] {});
+            }
+        }
+    };
+
+    // The ring's loads and refills are unconditional (a refill past the last blob re-reads the last
+    // blob's slice): a load on one side of a branch makes hipcc's counter state at the join treat it as
+    // the newest, and the slot's use then waits for every load in flight.
+    uint4 ring[DEPTH];
+    static_for<0, DEPTH>([&](auto u) {
+        const Slice S = slice((uint64_t)u < n_blobs ? (uint64_t)u : n_blobs - 1);
+        ring[u] = load_word(S.wa, S.nw, 0);
+    });
+    uint64_t b0 = 0;
+    for (; b0 + DEPTH <= n_blobs; b0 += DEPTH) {
+        static_for<0, DEPTH>([&](auto u) {
+            const uint64_t nb = b0 + u + DEPTH;
+            blob(b0 + u, ring[u], true, nb < n_blobs ? nb : n_blobs - 1);
+        });
+    }
+    static_for<0, DEPTH>([&](auto u) {                  // the last n_blobs % DEPTH blobs
+        if (b0 + u < n_blobs) blob(b0 + u, ring[u], false, 0);
+    });
+    static_for<0, COLS>([&](auto c) {
+        if (tid + c * NT < tile) out[e0 + tid + c * NT] = acc[c];
+    });
+}
+
 // Irregular blobs: the reference loop, one lane per blob (only malformed streams get here).
 // With out == nullptr it only counts.
 __global__ void varint_sequential_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ blob_off,
@@ -355,7 +634,7 @@ __global__ void varint_sequential_kernel(const uint8_t* __restrict__ bytes, cons
                                          uint64_t* __restrict__ blob_count, int64_t* __restrict__ out,
                                          uint64_t out_stride, uint64_t cap) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= n_blobs || !blob_irregular[b]) return;
+    if (b >= n_blobs || !(blob_irregular[b] & 1u)) return;
     uint64_t r = blob_off[b];
     const uint64_t e = blob_off[b + 1];
     uint64_t c = 0;
@@ -590,6 +869,7 @@ void varint_plan(const uint64_t* blob_off, uint64_t n_blobs, VarintPlan* plan) {
 struct DecodeWork {
     uint32_t* region_count; uint64_t* region_base;
     uint64_t* blob_off; uint64_t* blob_region; uint32_t* irregular; uint64_t* blob_count; uint32_t* wide;
+    uint16_t* sub_count;
 };
 static DecodeWork carve(void* work, size_t R, uint64_t n_blobs) {
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -601,16 +881,22 @@ static DecodeWork carve(void* work, size_t R, uint64_t n_blobs) {
     w.blob_region = (uint64_t*)p; p += up((n_blobs + 1) * 8);
     w.irregular = (uint32_t*)p; p += up(n_blobs * 4);
     w.blob_count = (uint64_t*)p; p += up(n_blobs * 8);
-    w.wide = (uint32_t*)p;
+    w.wide = (uint32_t*)p; p += 256;
+    w.sub_count = (uint16_t*)p;
     return w;
 }
 size_t varint_decode_work_bytes(size_t regions, uint64_t n_blobs) {
-    return regions * 12 + (n_blobs + 1) * 16 + n_blobs * 12 + 8 * 256;    // (7 x 256 B of rounding + flag)
+    // (7 x 256 B of rounding + flag) + the sub-chunk counts of the fused decode -> combine
+    return regions * 12 + (n_blobs + 1) * 16 + n_blobs * 12 + 8 * 256 + regions * 2 * kSubPerRegion;
 }
+uint64_t varint_tile_plan_bytes(uint64_t n_blobs, uint64_t dim) {
+    return n_blobs * ((dim + kDcTile - 1) / kDcTile) * 8;
+}
+uint64_t varint_fused_tiles(uint64_t dim) { return (dim + kDcTile - 1) / kDcTile; }
 
 hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
                                const VarintPlan& plan, void* work, uint64_t* counts_host, bool* irregular_any,
-                               hipStream_t s) {
+                               hipStream_t s, bool sub_counts, bool* long_any) {
     const size_t R = plan.regions;
     DecodeWork w = carve(work, R, n_blobs);
     hipError_t e;
@@ -620,7 +906,8 @@ hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_ho
     for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
         const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
         hipLaunchKernelGGL(varint_count_kernel, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s, bytes,
-                           w.blob_region, w.blob_off, (uint32_t)y0, w.region_count, w.irregular);
+                           w.blob_region, w.blob_off, (uint32_t)y0, w.region_count, w.irregular,
+                           sub_counts ? w.sub_count : nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(varint_scan_kernel, dim3((unsigned)n_blobs), dim3(kThreads), 0, s, w.region_count,
@@ -634,7 +921,12 @@ hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_ho
     if ((e = hipMemcpyAsync(irr.data(), w.irregular, n_blobs * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     *irregular_any = false;
-    for (uint64_t b = 0; b < n_blobs; ++b) *irregular_any |= irr[b] != 0;
+    bool lng = false;
+    for (uint64_t b = 0; b < n_blobs; ++b) {
+        *irregular_any |= (irr[b] & 1u) != 0;
+        lng |= (irr[b] & 2u) != 0;
+    }
+    if (long_any) *long_any = lng;
     return hipSuccess;
 }
 
@@ -677,6 +969,43 @@ hipError_t launch_varint_decode_narrow(const uint8_t* bytes, uint64_t n_blobs, c
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     *wide_host = flag != 0;
     return hipSuccess;
+}
+
+hipError_t launch_varint_decode_combine(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
+                                        uint64_t* tile_plan, uint64_t dim, int64_t* out, int64_t modulus,
+                                        bool multi, hipStream_t s) {
+    if (dim == 0 || n_blobs == 0) return hipSuccess;
+    const size_t R = plan.regions;
+    DecodeWork w = carve(work, R, n_blobs);
+    const uint64_t ntiles = varint_fused_tiles(dim);
+    if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipError_t e;
+    for (uint64_t y0 = 0; y0 < n_blobs; y0 += 65535) {
+        const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
+        hipLaunchKernelGGL(varint_tile_plan_kernel, dim3((unsigned)((plan.max_regions + kThreads - 1) / kThreads), ny),
+                           dim3(kThreads), 0, s, w.blob_off, w.blob_region, w.region_base, w.sub_count, (uint32_t)y0,
+                           n_blobs, ntiles, tile_plan);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    const Mod64 M = make_mod64(modulus);
+    const bool small_m = modulus <= ((int64_t)1 << 62);
+    const char* env = getenv("SDA_DC_DEPTH");                  // A/B knob: blobs prefetched ahead
+    const int depth = env ? atoi(env) : 4;
+    const dim3 grid((unsigned)ntiles), block(kDcThreads);
+    const uint64_t* tp = tile_plan;
+    if (multi)
+        hipLaunchKernelGGL((varint_decode_combine_kernel<2, true>), grid, block, 0, s, bytes, w.blob_off, n_blobs,
+                           tp, ntiles, dim, out, M, small_m);
+    else if (depth == 2)
+        hipLaunchKernelGGL((varint_decode_combine_kernel<2, false>), grid, block, 0, s, bytes, w.blob_off, n_blobs,
+                           tp, ntiles, dim, out, M, small_m);
+    else if (depth == 8)
+        hipLaunchKernelGGL((varint_decode_combine_kernel<8, false>), grid, block, 0, s, bytes, w.blob_off, n_blobs,
+                           tp, ntiles, dim, out, M, small_m);
+    else
+        hipLaunchKernelGGL((varint_decode_combine_kernel<4, false>), grid, block, 0, s, bytes, w.blob_off, n_blobs,
+                           tp, ntiles, dim, out, M, small_m);
+    return hipGetLastError();
 }
 
 size_t varint_encode_work_bytes(uint64_t rows, uint64_t len) {

@@ -699,7 +699,8 @@ namespace {
 
 // Plan + count N device-resident blobs; counts[n] on the host.
 sda_status codec_count(sda_engine* h, const uint8_t* bytes, const uint64_t* blob_off, uint64_t n_blobs,
-                       sda::VarintPlan* plan, uint64_t* counts, bool* irregular, hipStream_t st) {
+                       sda::VarintPlan* plan, uint64_t* counts, bool* irregular, hipStream_t st,
+                       bool sub_counts = false, bool* long_any = nullptr) {
     if (((uintptr_t)bytes & 15) != 0) return fail(SDA_ERR_INVALID_ARGUMENT, "byte buffer must be 16-byte aligned");
     for (uint64_t b = 0; b < n_blobs; ++b)
         if (blob_off[b + 1] < blob_off[b]) return fail(SDA_ERR_INVALID_ARGUMENT, "blob offsets must be non-decreasing");
@@ -707,7 +708,8 @@ sda_status codec_count(sda_engine* h, const uint8_t* bytes, const uint64_t* blob
     if (sda_status e = ensure(&h->codec_work, &h->codec_work_bytes,
                               sda::varint_decode_work_bytes(plan->regions, n_blobs)))
         return e;
-    HIP_TRY(sda::launch_varint_count(bytes, blob_off, n_blobs, *plan, h->codec_work, counts, irregular, st));
+    HIP_TRY(sda::launch_varint_count(bytes, blob_off, n_blobs, *plan, h->codec_work, counts, irregular, st,
+                                     sub_counts, long_any));
     return SDA_OK;
 }
 
@@ -716,10 +718,16 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
                           int64_t* out, uint64_t out_cap, uint64_t* out_len, hipStream_t st) {
     *out_len = 0;
     if (n_blobs == 0) return ok();                                  // combiner.rs:17: empty input
+    // SDA_CODEC_PATH (A/B and test knob): "fused" (every size) or "matrix"; default: fused from 256
+    // column tiles up (below that the per-tile blob walk is too short of workgroups to fill the chip)
+    const char* path = getenv("SDA_CODEC_PATH");
+    const bool force_matrix = path && strcmp(path, "matrix") == 0, force_fused = path && strcmp(path, "fused") == 0;
     sda::VarintPlan plan;
     std::vector<uint64_t> counts(n_blobs);
-    bool irregular = false;
-    if (sda_status e = codec_count(h, bytes, blob_off, n_blobs, &plan, counts.data(), &irregular, st)) return e;
+    bool irregular = false, long_elems = false;
+    if (sda_status e = codec_count(h, bytes, blob_off, n_blobs, &plan, counts.data(), &irregular, st, !force_matrix,
+                                   &long_elems))
+        return e;
     const uint64_t dim = counts[0];
     for (uint64_t i = 1; i < n_blobs; ++i)
         if (counts[i] != dim)
@@ -732,6 +740,14 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
     if (out_cap < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
     *out_len = dim;
     if (dim == 0) return ok();
+    if (!irregular && !force_matrix && (force_fused || sda::varint_fused_tiles(dim) >= 256)) {
+        // one pass over the payload: no [N][dim] matrix (the matrix buffer holds the tile plan)
+        if (sda_status e = ensure(&h->codec_mat, &h->codec_mat_bytes, sda::varint_tile_plan_bytes(n_blobs, dim)))
+            return e;
+        HIP_TRY(sda::launch_varint_decode_combine(bytes, n_blobs, plan, h->codec_work,
+                                                  static_cast<uint64_t*>(h->codec_mat), dim, out, mm, long_elems, st));
+        return SDA_OK;
+    }
     if (sda_status e = ensure(&h->codec_mat, &h->codec_mat_bytes, n_blobs * dim * 8)) return e;
     // Decoded field shares fit in int32 (|share| < m <= 2^31 for every field the reference uses): the
     // [N][dim] matrix between the decode and the combine is stored narrowed, which halves its write and

@@ -102,10 +102,11 @@ struct VarintPlan {
 };
 void varint_plan(const uint64_t* blob_off, uint64_t n_blobs, VarintPlan* plan);
 size_t varint_decode_work_bytes(size_t regions, uint64_t n_blobs);
-// element count of every blob (synchronous: copies n_blobs counts to the host)
+// element count of every blob (synchronous: copies n_blobs counts to the host); long_any: some element
+// has >= 6 bytes (sub_counts: also the 256-byte sub-chunk counts of the fused decode -> combine)
 hipError_t launch_varint_count(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
                                const VarintPlan& plan, void* work, uint64_t* counts_host, bool* irregular_any,
-                               hipStream_t s);
+                               hipStream_t s, bool sub_counts = false, bool* long_any = nullptr);
 // decode every blob into out + blob * out_stride (after launch_varint_count on the same work)
 hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
                                 int64_t* out, uint64_t out_stride, uint64_t len, bool irregular_any,
@@ -114,6 +115,14 @@ hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const Va
 // (synchronous) tells whether some value did not fit, in which case out holds garbage
 hipError_t launch_varint_decode_narrow(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
                                        int32_t* out, uint64_t out_stride, bool* wide_host, hipStream_t s);
+// The clerk's fused decode -> combine (after launch_varint_count with sub_counts on the same work; regular
+// blobs of equal element count dim): out[dim] = combiner.rs:16-28 over the decoded blobs in order, each
+// payload read once.  tile_plan: device scratch of varint_tile_plan_bytes(n_blobs, dim).
+uint64_t varint_tile_plan_bytes(uint64_t n_blobs, uint64_t dim);
+uint64_t varint_fused_tiles(uint64_t dim);
+hipError_t launch_varint_decode_combine(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
+                                        uint64_t* tile_plan, uint64_t dim, int64_t* out, int64_t modulus,
+                                        bool multi, hipStream_t s);
 size_t varint_encode_work_bytes(uint64_t rows, uint64_t len);
 // encode rows [rows][stride] (first len elements) back to back into dst; row_bytes_host gets each
 // row's byte count (synchronous).  hipErrorInvalidValue if dst_cap is too small.
