@@ -20,8 +20,9 @@
 // Irregular blobs (malformed streams) are decoded by a sequential exact kernel instead.
 // Roofline: HBM.  Algorithmic bytes = payload bytes read + 8 B per decoded element written.
 //
-// The clerk's decode -> combine (clerk.rs:79-86) fuses pass C with the combine instead of writing a
-// [N][len] matrix: pass A also counts the terminators of every 256-byte sub-chunk; a plan kernel
+// The clerk's decode -> combine (clerk.rs:79-86) decodes into an int32 matrix and runs the exact combine.
+// An opt-in variant (SDA_CODEC_PATH=fused; measured slower -- VALU-bound, profiles/r02d/ab_codec_fused.txt)
+// fuses pass C with the combine instead of writing the [N][len] matrix: pass A also counts the terminators of every 256-byte sub-chunk; a plan kernel
 // locates, per (column tile of kDcTile elements, blob), the sub-chunk holding the terminator that ends
 // the previous tile and how many of its terminators precede the tile; then one workgroup per column
 // tile walks the blobs in order, decodes its tile's slice of each payload (read once, plus at most a

@@ -718,10 +718,11 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
                           int64_t* out, uint64_t out_cap, uint64_t* out_len, hipStream_t st) {
     *out_len = 0;
     if (n_blobs == 0) return ok();                                  // combiner.rs:17: empty input
-    // SDA_CODEC_PATH (A/B and test knob): "fused" (every size) or "matrix"; default: fused from 256
-    // column tiles up (below that the per-tile blob walk is too short of workgroups to fill the chip)
+    // SDA_CODEC_PATH=fused (A/B and test knob) runs the column-tile decode+combine, which reads the payload
+    // once instead of writing and re-reading an int32 matrix but measured slower (VALU-bound: 3.4 ms per
+    // 1000 x 1M launch vs 2.2 + 0.7 ms, profiles/r02d/ab_codec_fused.txt); the default is the matrix path.
     const char* path = getenv("SDA_CODEC_PATH");
-    const bool force_matrix = path && strcmp(path, "matrix") == 0, force_fused = path && strcmp(path, "fused") == 0;
+    const bool force_fused = path && strcmp(path, "fused") == 0, force_matrix = !force_fused;
     sda::VarintPlan plan;
     std::vector<uint64_t> counts(n_blobs);
     bool irregular = false, long_elems = false;
@@ -740,7 +741,7 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
     if (out_cap < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
     *out_len = dim;
     if (dim == 0) return ok();
-    if (!irregular && !force_matrix && (force_fused || sda::varint_fused_tiles(dim) >= 256)) {
+    if (!irregular && force_fused) {
         // one pass over the payload: no [N][dim] matrix (the matrix buffer holds the tile plan)
         if (sda_status e = ensure(&h->codec_mat, &h->codec_mat_bytes, sda::varint_tile_plan_bytes(n_blobs, dim)))
             return e;

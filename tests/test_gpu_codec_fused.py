@@ -3,13 +3,15 @@ the oracle: clerk.rs:79-86 decodes every decrypted participation (sodium.rs:82-8
 VarInt) and folds it into ShareCombiner::combine (combiner.rs:16-28), exact and order-dependent for
 signed shares.  Bit-exact.
 
-The fused path walks column tiles of 1,024 elements; its plan locates each tile's first element in
+The fused path walks column tiles of 1,536 elements; its plan locates each tile's first element in
 every payload through the count pass's 256-byte sub-chunk counts.  The cases below put tile edges on
 every kind of byte position: element lengths 1..10 (zeros, field shares, full-range i64), dimensions
-either side of a tile, payloads at unaligned offsets, truncated final varints, slices longer than one
-round (10-byte elements), and moduli from 1 to i64::MAX (negative ones as |m|, as Rust's `%`).
-`SDA_CODEC_PATH=fused` forces the path at every size (by default it starts at 256 tiles) and
-`=matrix` the decode-to-matrix + combine path it replaces, which must agree.
+either side of a tile, payloads at unaligned offsets, truncated final varints, jobs with elements of
+>= 6 bytes (the multi-round variant, slices longer than one word per lane), and moduli from 1 to
+i64::MAX (negative ones as |m|, as Rust's `%`).
+`SDA_CODEC_PATH=fused` selects it (it measured slower than the default decode-to-int32-matrix + combine,
+profiles/r02d/ab_codec_fused.txt, so it is opt-in); `=matrix` (or unset) is the default path.  Both must
+agree with the oracle on every case.
 """
 import numpy as np
 import pytest
@@ -50,7 +52,7 @@ def _rows(rng, kind, n, d):
         return np.zeros((n, d), np.int64)
     if kind == "small":
         return rng.integers(-64, 64, size=(n, d), dtype=np.int64)
-    if kind == "wide":                                     # 10-byte elements: slices of 2+ rounds
+    if kind == "wide":                                     # 10-byte elements: slices of 2+ rounds (multi)
         return rng.choice(np.array([I64_MIN, I64_MAX, I64_MIN + 1, -(2**62) - 7, 2**63 - 9], np.int64), size=(n, d))
     # mixed lengths 1..10, a different pattern per row
     k = rng.integers(0, 4, size=(n, d))
@@ -61,7 +63,7 @@ def _rows(rng, kind, n, d):
 
 
 @pytest.mark.parametrize("kind", ["field", "zeros", "small", "wide", "mixed"])
-@pytest.mark.parametrize("dim", [1, 2, 1023, 1024, 1025, 2048, 5003])
+@pytest.mark.parametrize("dim", [1, 2, 1535, 1536, 1537, 3072, 5003])
 def test_fused_decode_combine_shapes(engine, oracle, monkeypatch, kind, dim):
     rng = np.random.default_rng(dim * 7 + len(kind))
     n = 5 if kind in ("wide", "mixed") else 9
@@ -96,7 +98,7 @@ def test_fused_decode_combine_truncated_tails(engine, oracle, monkeypatch):
 
 def test_fused_decode_combine_many_blobs_ragged_offsets(engine, oracle, monkeypatch):
     """100 participations with different byte lengths (unaligned offsets), more blobs than one prefetch
-    ring and a dimension past 16 KiB regions; the default path choice (fused from 256 tiles up) agrees"""
+    ring and a dimension past 16 KiB regions"""
     rng = np.random.default_rng(12)
     D = 12_345
     x = np.concatenate([_rows(rng, "field", 60, D), _rows(rng, "mixed", 25, D), _rows(rng, "zeros", 15, D)])
@@ -107,10 +109,9 @@ def test_fused_decode_combine_many_blobs_ragged_offsets(engine, oracle, monkeypa
     assert_same(_run(engine, M31, blobs, D, "matrix", monkeypatch), exp)
 
 
-def test_fused_decode_combine_default_at_scale(engine, oracle, monkeypatch):
-    """64 x 400,003 field shares on the device (encode_dev -> decode+combine_dev): the default path is the
-    fused one here (391 tiles); equal to the oracle's combine on every column"""
-    monkeypatch.delenv("SDA_CODEC_PATH", raising=False)
+def test_fused_decode_combine_at_scale(engine, oracle, monkeypatch):
+    """64 x 400,003 field shares on the device (encode_dev -> decode+combine_dev), both paths, equal to the
+    oracle's combine on every column"""
     N, D = 64, 400_003
     x = torch.empty((N, D), dtype=torch.int64, device="cuda")
     engine.synth_fill_dev(x.data_ptr(), N, D, 0xF05ED, -(M31 - 1), M31)
@@ -118,10 +119,13 @@ def test_fused_decode_combine_default_at_scale(engine, oracle, monkeypatch):
     buf = torch.zeros(cap, dtype=torch.uint8, device="cuda")
     row_bytes = engine.varint_encode_dev(x.data_ptr(), N, D, D, buf.data_ptr(), cap)
     off = np.concatenate([[0], np.cumsum(row_bytes)]).astype(np.uint64)
-    out = torch.empty(D, dtype=torch.int64, device="cuda")
-    assert engine.clerk_decode_combine_dev(M31, buf.data_ptr(), off, out.data_ptr(), D) == D
-    torch.cuda.synchronize()
-    assert_same(out.cpu().numpy(), oracle.combine(M31, x.cpu().numpy()))
+    exp = oracle.combine(M31, x.cpu().numpy())
+    for path in ("fused", "matrix"):
+        monkeypatch.setenv("SDA_CODEC_PATH", path)
+        out = torch.full((D,), 7, dtype=torch.int64, device="cuda")
+        assert engine.clerk_decode_combine_dev(M31, buf.data_ptr(), off, out.data_ptr(), D) == D
+        torch.cuda.synchronize()
+        assert_same(out.cpu().numpy(), exp, path)
 
 
 def test_fused_decode_combine_irregular_falls_back(engine, oracle, monkeypatch):
