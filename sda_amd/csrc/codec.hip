@@ -22,8 +22,9 @@
 //
 // The clerk's decode -> combine (clerk.rs:79-86) decodes into an int32 matrix and runs the exact combine.
 // An opt-in variant (SDA_CODEC_PATH=fused; measured slower -- VALU-bound, profiles/r02d/ab_codec_fused.txt)
-// fuses pass C with the combine instead of writing the [N][len] matrix: pass A also counts the terminators of every 256-byte sub-chunk; a plan kernel
-// locates, per (column tile of kDcTile elements, blob), the sub-chunk holding the terminator that ends
+// fuses pass C with the combine instead of writing the [N][len] matrix: pass A also counts the
+// terminators of every 256-byte sub-chunk; a plan kernel locates, per (column tile of kDcTile
+// elements, blob), the sub-chunk holding the terminator that ends
 // the previous tile and how many of its terminators precede the tile; then one workgroup per column
 // tile walks the blobs in order, decodes its tile's slice of each payload (read once, plus at most a
 // sub-chunk per tile edge) and folds it into combiner.rs:16-28's exact recurrence in registers.
