@@ -297,9 +297,12 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
     uint64_t r, word;
     if (!region_of(blob_region, blob_off, y0, &b, &r, &word) || (blob_irregular[b] & 1u)) return;
     __shared__ uint32_t lb[(kRegionBytes + 32) / 4];          // [halo 16 B | region 16 KiB | tail 16 B]
-    __shared__ uint32_t cml[kWPT * kThreads + 1];             // continuation mask of lb word w at [w]
+    __shared__ uint16_t cml[kWPT * kThreads + 1];             // continuation mask (16 bits) of lb word w at [w]
     __shared__ uint32_t wsum[kThreads / 64];
-    __shared__ uint32_t el[kSubBytes];                        // one sub-region's elements: start | len << 16
+    // one sub-region's element starts (byte positions in lb, < 2^15) and, after the last, its end: an
+    // element ends where the next one starts (the blob's elements are contiguous), so a u16 per element
+    // suffices -- 8 KiB instead of 16, which lets 5 workgroups share a CU's LDS instead of 4
+    __shared__ uint16_t el[kSubBytes + 1];
     const uint64_t begin = blob_off[b], end = blob_off[b + 1];
     // every window of the region inside the blob, and the blob's last byte past the region
     const bool interior = word * 16 >= begin + 16 && end > word * 16 + kRegionBytes;
@@ -328,7 +331,7 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
 #pragma unroll
     for (int k = 0; k < kWPT; ++k) {
         const uint32_t wl = threadIdx.x + k * kThreads;
-        const uint32_t cm = cml[wl] | (cml[wl + 1] << 16);
+        const uint32_t cm = (uint32_t)cml[wl] | ((uint32_t)cml[wl + 1] << 16);
         W[k] = interior ? interior_window(cm) : make_window_cm(cm, word + wl, begin, end);
     }
     OutT* dst = out + (uint64_t)b * out_stride + region_base[r];
@@ -359,15 +362,16 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
             do {
                 const uint32_t j = __builtin_ctz(rem);
                 rem &= rem - 1;
-                el[e++] = (pos0 + st) | ((j - st + 1) << 16);
+                el[e++] = (uint16_t)(pos0 + st);
                 st = j + 1;
             } while (rem);
+            if (e == total) el[total] = (uint16_t)(pos0 + st);    // end of the sub-region's last element
         }
         __syncthreads();
         // 2. decode: lane i takes element i -> balanced work, coalesced stores
         for (uint32_t i = threadIdx.x; i < total; i += kThreads) {
-            const uint32_t P = el[i] & 0xFFFFu;                  // byte position in lb
-            const uint32_t len = el[i] >> 16;                     // 1..11 on regular blobs
+            const uint32_t P = el[i];                             // byte position in lb
+            const uint32_t len = el[i + 1] - P;                   // 1..11 on regular blobs
             if constexpr (sizeof(OutT) < 8) {
                 const uint32_t q = P >> 2, sh = (P & 3) * 8;
                 const uint32_t d0 = lb[q], d1 = lb[q + 1], d2 = lb[q + 2];
