@@ -274,14 +274,14 @@ __device__ __forceinline__ int64_t varint_value_at(const uint32_t* lb, uint32_t 
     return val;
 }
 
-// pass C: decode.  The region's bytes (plus a 16-byte halo on each side) are staged in LDS, with
-// each word's 16-bit continuation mask beside them (so a window's previous-word mask is one LDS
-// read).  The region is walked as kWPT sub-regions of one word per thread.  Per sub-region a
-// block-wide scan of the terminator counts compacts the elements' (start, length) into LDS; then
-// lane i decodes element i (balanced work, coalesced stores) from funnel-shifted dwords -- elements
-// of <= 5 bytes (every field share below 2^31) on a short 32-bit path, longer ones on the general
-// one.  Element index of a terminator = region base + terminators before it in the region.  Blobs
-// flagged irregular are skipped here (varint_sequential_kernel).
+// pass C: decode.  Each thread loads its kWPT words of the region up front (all in flight); the region
+// is then walked as kWPT sub-regions of one word per thread, each staged in LDS with a 16-byte halo
+// (the previous word) and every word's 16-bit continuation mask beside it.  Per sub-region a
+// block-wide scan of the terminator counts compacts the elements' starts into LDS; then lane i decodes
+// element i (balanced work, coalesced stores) from funnel-shifted dwords -- elements of <= 5 bytes
+// (every field share below 2^31) on a short 32-bit path, longer ones on the general one.  Element
+// index of a terminator = region base + terminators before it in the region.  Blobs flagged irregular
+// are skipped here (varint_sequential_kernel).
 //
 // OutT = int32_t (the clerk's decode -> combine of field shares, |v| < 2^31): the values are stored
 // narrowed and any value that does not fit sets *wide (the caller then decodes again as i64).
@@ -296,56 +296,48 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
     uint32_t b;
     uint64_t r, word;
     if (!region_of(blob_region, blob_off, y0, &b, &r, &word) || (blob_irregular[b] & 1u)) return;
-    __shared__ uint32_t lb[(kRegionBytes + 32) / 4];          // [halo 16 B | region 16 KiB | tail 16 B]
-    __shared__ uint16_t cml[kWPT * kThreads + 1];             // continuation mask (16 bits) of lb word w at [w]
+    // LDS holds one sub-region at a time (the region's other words wait in registers): 12.9 KB per
+    // workgroup instead of 26.7, so LDS no longer caps the waves per SIMD
+    __shared__ uint32_t lb[(kSubBytes + 32) / 4];             // [halo 16 B | sub-region 4 KiB | tail 16 B]
+    __shared__ uint16_t cml[kThreads + 1];                    // continuation mask (16 bits) of lb word w at [w]
     __shared__ uint32_t wsum[kThreads / 64];
-    // one sub-region's element starts (byte positions in lb, < 2^15) and, after the last, its end: an
-    // element ends where the next one starts (the blob's elements are contiguous), so a u16 per element
-    // suffices -- 8 KiB instead of 16, which lets 5 workgroups share a CU's LDS instead of 4
+    // one sub-region's element starts (byte positions in lb) and, after the last, its end: an element
+    // ends where the next one starts (the blob's elements are contiguous), so a u16 per element suffices
     __shared__ uint16_t el[kSubBytes + 1];
+    uint4* lb4 = reinterpret_cast<uint4*>(lb);
     const uint64_t begin = blob_off[b], end = blob_off[b + 1];
     // every window of the region inside the blob, and the blob's last byte past the region
     const bool interior = word * 16 >= begin + 16 && end > word * 16 + kRegionBytes;
-    {
-        const uint4* p = reinterpret_cast<const uint4*>(bytes);
-        uint4 v[kWPT];
-#pragma unroll
-        for (int k = 0; k < kWPT; ++k) {
-            const uint64_t wk = word + threadIdx.x + k * kThreads;
-            v[k] = wk * 16 < end ? p[wk] : make_uint4(0, 0, 0, 0);
-        }
-        if (threadIdx.x == 0) {
-            const uint4 h = (word * 16 > begin) ? p[word - 1] : make_uint4(0, 0, 0, 0);
-            reinterpret_cast<uint4*>(lb)[0] = h;
-            cml[0] = cont_mask(h);
-        }
-        if (threadIdx.x == kThreads - 1) reinterpret_cast<uint4*>(lb)[kWPT * kThreads + 1] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < kWPT; ++k) {
-            reinterpret_cast<uint4*>(lb)[threadIdx.x + k * kThreads + 1] = v[k];
-            cml[threadIdx.x + k * kThreads + 1] = cont_mask(v[k]);
-        }
-    }
-    __syncthreads();
-    Window W[kWPT];
+    const uint4* p = reinterpret_cast<const uint4*>(bytes);
+    uint4 v[kWPT];
 #pragma unroll
     for (int k = 0; k < kWPT; ++k) {
-        const uint32_t wl = threadIdx.x + k * kThreads;
-        const uint32_t cm = (uint32_t)cml[wl] | ((uint32_t)cml[wl + 1] << 16);
-        W[k] = interior ? interior_window(cm) : make_window_cm(cm, word + wl, begin, end);
+        const uint64_t wk = word + threadIdx.x + k * kThreads;
+        v[k] = wk * 16 < end ? p[wk] : make_uint4(0, 0, 0, 0);
     }
+    uint4 h = make_uint4(0, 0, 0, 0);                         // the word before the region (thread 0)
+    if (threadIdx.x == 0 && word * 16 > begin) h = p[word - 1];
+    if (threadIdx.x == kThreads - 1) lb4[kThreads + 1] = make_uint4(0, 0, 0, 0);
     OutT* dst = out + (uint64_t)b * out_stride + region_base[r];
     bool narrow_fail = false;
     uint32_t base = 0;                                        // elements in earlier sub-regions
 #pragma unroll
     for (int k = 0; k < kWPT; ++k) {
-        // 1. compaction: each thread lists the (start, length) of the elements ending in its word
-        const uint32_t tm = W[k].term & W[k].valid;
+        const uint32_t wl = threadIdx.x + k * kThreads;
+        const uint32_t cmk = cont_mask(v[k]);
+        // terminators of the own word (they do not depend on the previous word) and their block scan
+        const Window Wo = interior ? interior_window(cmk << 16) : make_window_cm(cmk << 16, word + wl, begin, end);
+        const uint32_t tm = Wo.term & Wo.valid;
         const uint32_t n = __builtin_popcount(tm);
-        const uint32_t incl = wave_incl_scan(n);              // exclusive scan of n over the block
-        __syncthreads();                                      // lb visible; el / wsum free for reuse
+        const uint32_t incl = wave_incl_scan(n);
+        if (k > 0) __syncthreads();                           // the previous sub-region's decode is done
+        lb4[threadIdx.x + 1] = v[k];
+        cml[threadIdx.x + 1] = (uint16_t)cmk;
+        if (k == 0 && threadIdx.x == 0) { lb4[0] = h; cml[0] = (uint16_t)cont_mask(h); }
+        if (k > 0 && threadIdx.x == kThreads - 1) { lb4[0] = v[k - 1]; cml[0] = (uint16_t)cont_mask(v[k - 1]); }
         if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
         __syncthreads();
+        // 1. compaction: each thread lists the starts of the elements ending in its word
         uint32_t e = incl - n, total = 0;
         for (uint32_t w = 0; w < kThreads / 64; ++w) {
             if (w < (threadIdx.x >> 6)) e += wsum[w];
@@ -354,8 +346,10 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
         if (tm) {
             // the first element starts after the previous boundary (a terminator, or a byte outside
             // the blob); each later one right after the terminator before it
-            const uint32_t boundary = W[k].term | ~(W[k].term | W[k].cont);
-            const uint32_t pos0 = (threadIdx.x + k * kThreads) * 16;
+            const uint32_t cm = (uint32_t)cml[threadIdx.x] | (cmk << 16);
+            const Window W = interior ? interior_window(cm) : make_window_cm(cm, word + wl, begin, end);
+            const uint32_t boundary = W.term | ~(W.term | W.cont);
+            const uint32_t pos0 = threadIdx.x * 16;
             uint32_t rem = tm;
             const uint32_t below = boundary & ((1u << __builtin_ctz(rem)) - 1u);
             uint32_t st = below ? 32 - __builtin_clz(below) : 0;      // window index of the first byte
