@@ -160,12 +160,25 @@ __global__ __launch_bounds__(kThreads) void varint_count_kernel(const uint8_t* _
     }
     uint4 halo = make_uint4(0, 0, 0, 0);
     if (threadIdx.x == 0 && word * 16 > begin) halo = p[word - 1];
-    Window W[kWPT];
+    // every word of the region inside the blob and the blob's last byte past it (most regions): the
+    // masks need no blob-edge clipping
+    const bool interior = word * 16 >= begin + 16 && end > word * 16 + kRegionBytes;
+    uint32_t term[kWPT], cont[kWPT], valid[kWPT];        // 16-bit masks of the own word
 #pragma unroll
     for (int k = 0; k < kWPT; ++k) {
         const uint32_t wl = threadIdx.x + k * kThreads;
-        W[k] = make_window(make_uint4(0, 0, 0, 0), v[k], word + wl, begin, end);   // own-word masks only
-        cm_l[wl + 1] = W[k].cont >> 16;
+        const uint32_t cm = cont_mask(v[k]);
+        if (interior) {
+            term[k] = ~cm & 0xFFFFu;
+            cont[k] = cm;
+            valid[k] = 0xFFFFu;
+        } else {
+            const Window W = make_window_cm(cm << 16, word + wl, begin, end);
+            term[k] = (W.term & W.valid) >> 16;
+            cont[k] = W.cont >> 16;
+            valid[k] = W.valid >> 16;
+        }
+        cm_l[wl + 1] = cont[k];
     }
     if (threadIdx.x == 0) cm_l[0] = make_window(make_uint4(0, 0, 0, 0), halo, word - 1, begin, end).cont >> 16;
     __syncthreads();
@@ -173,22 +186,19 @@ __global__ __launch_bounds__(kThreads) void varint_count_kernel(const uint8_t* _
 #pragma unroll
     for (int k = 0; k < kWPT; ++k) {
         const uint32_t wl = threadIdx.x + k * kThreads;
-        const uint32_t nk = __builtin_popcount(W[k].term & W[k].valid);
+        const uint32_t nk = __builtin_popcount(term[k]);
         n += nk;
         if (sub_count) {
             const uint32_t rs = row16_incl_scan(nk);
             if ((threadIdx.x & 15) == 15) sub_count[r * kSubPerRegion + (wl >> 4)] = (uint16_t)rs;
         }
-        // 11 continuation bytes in a row ending inside this word?
-        const uint32_t cont = W[k].cont | cm_l[wl];
-        uint32_t run = cont, run5 = 0;
-#pragma unroll
-        for (int q = 1; q <= 10; ++q) {
-            run &= cont << q;
-            if (q == 4) run5 = run;                      // 5 continuation bytes: an element of >= 6 bytes
-        }
-        bad |= run & W[k].valid;
-        lng |= run5 & W[k].valid;
+        // runs of continuation bytes ending inside this word (bit j of rK: bytes j-K+1 .. j all continue):
+        // 11 in a row = an irregular blob, 5 = an element of >= 6 bytes
+        const uint32_t c = (cont[k] << 16) | cm_l[wl];
+        const uint32_t r2 = c & (c << 1), r4 = r2 & (r2 << 2), r5 = r4 & (c << 4);
+        const uint32_t r8 = r4 & (r4 << 4), r11 = r8 & (r4 << 7);
+        bad |= r11 & (valid[k] << 16);
+        lng |= r5 & (valid[k] << 16);
     }
     // bit 0: irregular (sequential decoder); bit 1: an element of >= 6 bytes (the fused decode -> combine
     // then takes its multi-round variant)
