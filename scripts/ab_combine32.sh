@@ -1,3 +1,4 @@
+# A/B record: the SDA_COMBINE32_UNROLL knob this compared was removed after the A/B (profiles/r02d/ab_combine32_unroll.txt)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
