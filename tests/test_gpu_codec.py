@@ -152,3 +152,39 @@ def test_clerk_decode_combine_narrow_and_wide(engine, oracle, monkeypatch, vec):
         torch.cuda.synchronize()
         assert_same(out.cpu().numpy(), oracle.combine(m, rows), name + " (int64)")
         monkeypatch.delenv("SDA_CODEC_NARROW")
+
+
+@pytest.mark.parametrize("run", [4, 5, 6, 10, 11, 12, 25])
+def test_continuation_runs_at_every_alignment(engine, oracle, monkeypatch, run):
+    """Runs of `run` continuation bytes placed at every byte offset of a 16-byte word (and across word
+    and 4 KiB sub-region boundaries): the count pass classifies a blob from them -- 11 in a row make it
+    irregular (sequential decoder, as u64::decode_var stops at shift > 70), 5 or more mark elements of
+    >= 6 bytes (the fused path's multi-round variant).  Both decode paths and both decode+combine paths
+    must equal the oracle whatever the alignment."""
+    rng = np.random.default_rng(100 + run)
+    m = 2147482801
+    S = 4200                                        # elements per blob (past one 4 KiB sub-region)
+    rows, blobs = [], []
+    for shift in list(range(0, 34)) + [4070, 4085, 4090, 4095, 4100]:
+        pre = bytes(shift)                          # `shift` one-byte zeros
+        mid = bytes([0xFF] * run + [0x01])
+        base = oracle.varint_decode(pre + mid)      # the run's element(s) as the reference decodes them
+        tail = oracle.varint_encode(rng.integers(-(m - 1), m, size=S - base.size, dtype=np.int64))
+        blob = pre + mid + tail
+        r = oracle.varint_decode(blob)
+        assert r.size == S
+        rows.append(r)
+        blobs.append(blob)
+    rows = np.stack(rows)
+    t, off = _pack(blobs)
+    out = torch.full((len(blobs), S), 7, dtype=torch.int64, device="cuda")
+    counts = engine.varint_decode_dev(t.data_ptr(), off, out.data_ptr(), S)
+    assert counts.tolist() == [S] * len(blobs)
+    assert_same(out.cpu().numpy(), rows, f"decode run={run}")
+    exp = oracle.combine(m, rows)
+    for path in ("matrix", "fused"):
+        monkeypatch.setenv("SDA_CODEC_PATH", path)
+        res = torch.full((S,), 7, dtype=torch.int64, device="cuda")
+        assert engine.clerk_decode_combine_dev(m, t.data_ptr(), off, res.data_ptr(), S) == S
+        torch.cuda.synchronize()
+        assert_same(res.cpu().numpy(), exp, f"{path} run={run}")
