@@ -455,6 +455,9 @@ def main():
             "decode_hbm_GBps": (payload + 8.0 * Nc * Dc) / (d_ms * 1e-3) / 1e9,
             "decode_combine_ms": c_ms, "decode_combine_shares_per_s": Nc * Dc / (c_ms * 1e-3),
             "decode_combine_payload_GBps": payload / (c_ms * 1e-3) / 1e9,
+            # bytes the three passes move: payload read twice (count, decode), the int32 matrix written and
+            # read back, the i64 result written
+            "decode_combine_hbm_GBps": (2 * payload + 8.0 * Nc * Dc + 8.0 * Dc) / (c_ms * 1e-3) / 1e9,
             "decode_combine_path": "count pass, decode to an int32 matrix, exact combine",
             "decode_combine_fused_ms": cm_ms,
             "encode_ms": e_ms, "encode_hbm_GBps": (payload + 8.0 * Nc * Dc) / (e_ms * 1e-3) / 1e9,
