@@ -573,3 +573,51 @@ def test_packed_wide_domain_limits(engine):
     with pytest.raises(SdaError) as ei:
         engine.share_generate(S.PackedShamir(1000, 2186, 1047, 2147483647 - 12, 3, 5), [1], [0] * 1047)
     assert ei.value.status == E.ERR_UNSUPPORTED
+
+
+def _random_packed_scheme(rng):
+    """A random tss-valid scheme: k + t + 1 = L (power of 2), n + 1 = N3 (power of 3) with k + t <= n, a
+    random prime p = 1 mod lcm(L, N3) below 2^31 from one of three magnitude bands (so both the lazy and
+    the verbatim truncation paths run), and roots of unity from a random generator."""
+    L = int(rng.choice([2, 4, 8, 16, 32, 64]))
+    N3 = int(rng.choice([n3 for n3 in (3, 9, 27, 81) if n3 > L]))
+    k = int(rng.integers(1, L))
+    t = L - 1 - k
+    step = L * N3 // math.gcd(L, N3)
+    lo, hi = [(N3 + 2, 1 << 16), (1 << 16, 1 << 24), (1 << 24, 1 << 31)][int(rng.integers(0, 3))]
+    while True:
+        c = int(rng.integers(max(1, lo // step), (hi - 1) // step))
+        p = c * step + 1
+        if lo <= p < hi and all(p % q for q in range(2, int(p**0.5) + 1)):
+            break
+    ws, wn = _roots(p, L, N3)
+    e = int(rng.integers(1, p - 1))
+    while math.gcd(e, p - 1) != 1:
+        e += 1
+    return S.PackedShamir(k, N3 - 1, t, p, pow(ws, e, p), pow(wn, e, p))
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_packed_random_schemes(engine, oracle, seed):
+    """Random schemes (sizes, primes from 2^9 to 2^31, any primitive roots of the right orders):
+    share-gen with signed secrets in (-p, p) and reconstruct from random subsets of at least t + k
+    shares, against the oracle's tss restatement (bit-exact signed representatives)."""
+    rng = np.random.default_rng(0xC0FFEE + seed)
+    sch = _random_packed_scheme(rng)
+    p, n, k = sch.prime_modulus, sch.share_count, sch.secret_count
+    D = int(rng.integers(1, 300)) * k + int(rng.integers(0, k))
+    D = max(D, 1)
+    B = (D + k - 1) // k
+    secrets = rng.integers(-(p - 1), p, size=D, dtype=np.int64)
+    draws = rng.integers(0, p - 1, size=B * sch.privacy_threshold(), dtype=np.int64)
+    pp = _pp(oracle, sch)
+    shares = engine.share_generate(sch, secrets, draws)
+    assert_same(shares, oracle.packed_generate(pp, secrets, draws), f"gen {sch}")
+    need = sch.reconstruction_threshold()
+    for _ in range(3):
+        idx = rng.permutation(n)[:int(rng.integers(need, n + 1))].tolist()
+        got = engine.secret_reconstruct(sch, D, [(i, shares[i]) for i in idx])
+        rc, exp = oracle.packed_reconstruct(pp, D, idx, shares[idx])
+        assert rc == 0
+        assert_same(got, exp, f"reveal {sch} from {len(idx)}")
+        assert (got % p == secrets % p).all()
