@@ -621,3 +621,44 @@ def test_packed_random_schemes(engine, oracle, seed):
         assert rc == 0
         assert_same(got, exp, f"reveal {sch} from {len(idx)}")
         assert (got % p == secrets % p).all()
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_packed_wide_random_schemes(engine, oracle, seed):
+    """Random schemes past the register kernels (L up to 1024 over 243 or 729 points, primes from the
+    smallest valid one up to 2^31, random primitive roots): gen and reveal from random subsets (register
+    and workspace reveal paths) bit-exact vs the oracle."""
+    rng = np.random.default_rng(0xBEEF + seed)
+    N3 = int(rng.choice([243, 729]))
+    L = int(rng.choice([l for l in (2, 8, 64, 128, 256, 512, 1024) if l < N3]))
+    k = int(rng.integers(1, L))
+    t = L - 1 - k
+    step = L * N3
+    small = bool(rng.integers(0, 2))
+    lo, hi = (step + 1, 1 << 24) if small and step < (1 << 23) else (1 << 24, 1 << 31)
+    while True:
+        c = int(rng.integers(max(1, lo // step), (hi - 1) // step))
+        p = c * step + 1
+        if lo <= p < hi and all(p % q for q in range(2, int(p**0.5) + 1)):
+            break
+    ws, wn = _roots(p, L, N3)
+    e = int(rng.integers(1, p - 1))
+    while math.gcd(e, p - 1) != 1:
+        e += 1
+    sch = S.PackedShamir(k, N3 - 1, t, p, pow(ws, e, p), pow(wn, e, p))
+    n = sch.share_count
+    D = int(rng.integers(1, 4)) * k + int(rng.integers(0, k))
+    D = max(D, 1)
+    B = (D + k - 1) // k
+    secrets = rng.integers(-(p - 1), p, size=D, dtype=np.int64)
+    draws = rng.integers(0, p - 1, size=B * sch.privacy_threshold(), dtype=np.int64)
+    pp = _pp(oracle, sch)
+    shares = engine.share_generate(sch, secrets, draws)
+    assert_same(shares, oracle.packed_generate(pp, secrets, draws), f"gen {sch}")
+    need = sch.reconstruction_threshold()
+    for size in (need, int(rng.integers(need, n + 1))):
+        idx = rng.permutation(n)[:size].tolist()
+        got = engine.secret_reconstruct(sch, D, [(i, shares[i]) for i in idx])
+        rc, exp = oracle.packed_reconstruct(pp, D, idx, shares[idx])
+        assert rc == 0
+        assert_same(got, exp, f"reveal {sch} from {size}")
