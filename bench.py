@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--chacha-seeds", type=int, default=256)
     ap.add_argument("--no-side", action="store_true", help="skip packed-Shamir / ChaCha legs")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-signed-split", action="store_true",
+                    help="N > 1: skip the signed-shares leg of the participation split (two-pass path)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-check", action="store_true", help="A/B helper: skip the side-leg round-trip checks")
     ap.add_argument("--codec-rows", type=int, default=1000, help="participations in the codec leg")
@@ -128,7 +130,78 @@ def cpu_baseline(dim: int, budget_s: float):
             "single_core": {"value": round(one, 4), "unit": "GB/s", "cores": 1,
                             "sample": f"100 x {dim:,} rows, or_combine (the reference loop, 1 thread), "
                                       f"median of {n1} runs"},
+            "shamir": cpu_baseline_shamir(threads, budget_s),
+            "chacha": cpu_baseline_chacha(threads, budget_s),
             "host": host}
+
+
+def _median_time(fn, budget_s, runs=3):
+    """Median wall time of fn() over up to `runs` runs (at least 2) within about budget_s seconds."""
+    times = []
+    t_start = time.perf_counter()
+    while (len(times) < runs and (time.perf_counter() - t_start) < budget_s) or len(times) < 2:
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    return statistics.median(times), len(times)
+
+
+def _threaded(threads, jobs):
+    """Run the oracle calls in `jobs` on `threads` host threads (ctypes releases the GIL in the C code)."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        for f in [ex.submit(j) for j in jobs]:
+            f.result()
+
+
+def cpu_baseline_shamir(threads: int, budget_s: float):
+    """The second half of the metric on the host: oracle/sda_oracle.c's restatement of tss 0.2 share
+    (packed_shamir.rs:40-43 via batched.rs:19-53) and reconstruct (packed_shamir.rs:73-77 via
+    batched.rs:69-97) at configs[2]'s scheme, 1 core (the reference is single-threaded) and `threads`
+    cores (one participant vector per thread)."""
+    from oracle import oracle as O
+    from sda_amd import schemes as S
+    from sda_amd import synth
+    sch = S.CONFIG_PACKED
+    p, k, t, n = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count
+    pp = O.packed_params(k, n, t, p, sch.omega_secrets, sch.omega_shares)
+    Dg, Dr = 1_000_000, 250_000
+    vecs = max(1, threads)
+    sec = synth.fill(vecs, Dg, SEED_BASE + 2, 0, p)
+    drw = synth.fill(vecs, (Dg // k) * t, SEED_BASE + 22, 0, p - 1)
+    idx = list(range(n - (t + k), n))
+    shares = [O.packed_generate(pp, sec[v, :Dr], drw[v, :(Dr // k) * t])[idx] for v in range(vecs)]
+    g1, ng1 = _median_time(lambda: O.packed_generate(pp, sec[0], drw[0]), budget_s / 4)
+    ga, nga = _median_time(lambda: _threaded(threads, [lambda v=v: O.packed_generate(pp, sec[v], drw[v])
+                                                       for v in range(vecs)]), budget_s / 4)
+    r1, nr1 = _median_time(lambda: O.packed_reconstruct(pp, Dr, idx, shares[0]), budget_s / 4)
+    ra, nra = _median_time(lambda: _threaded(threads, [lambda v=v: O.packed_reconstruct(pp, Dr, idx, shares[v])
+                                                       for v in range(vecs)]), budget_s / 4)
+    B = Dg // k
+    return {"unit": "shares/s (gen), secrets/s (reveal)", "kind": "port",
+            "gen_shares_per_s": {"single_core": round(n * B / g1, 1), "all_cores": round(vecs * n * B / ga, 1),
+                                 "cores": threads},
+            "reveal_secrets_per_s": {"single_core": round(Dr / r1, 1), "all_cores": round(vecs * Dr / ra, 1),
+                                     "cores": threads, "clerks": len(idx)},
+            "sample": f"k=8 n=26 t=7 p={p}: share-gen of 1M-dim vectors (1 vector on 1 core, {vecs} on "
+                      f"{threads} threads), exact reveal of 250k-dim vectors from {len(idx)} clerks; "
+                      f"median of {ng1}/{nga}/{nr1}/{nra} runs; oracle/sda_oracle.c at -O2"}
+
+
+def cpu_baseline_chacha(threads: int, budget_s: float):
+    """chacha.rs:57-76 (MaskCombiner::combine) on the host: oracle/sda_oracle.c's rand-0.3 ChaChaRng +
+    gen_range restatement, seeds over 1M-dim; 1 core, and `threads` cores (seeds split over threads; every
+    draw is >= 0, so the per-thread canonical sums add exactly)."""
+    from oracle import oracle as O
+    D, per = 1_000_000, 2
+    seeds = (np.arange(threads * per * 4, dtype=np.int64).reshape(-1, 4) * 7919 + 13) % (1 << 31)
+    t1, n1 = _median_time(lambda: O.chacha_mask_combine(MODULUS, D, seeds[:per]), budget_s / 4)
+    ta, na = _median_time(lambda: _threaded(threads, [lambda i=i: O.chacha_mask_combine(
+        MODULUS, D, seeds[i * per:(i + 1) * per]) for i in range(threads)]), budget_s / 4)
+    return {"unit": "mask elements/s", "kind": "port", "single_core": round(per * D / t1, 1),
+            "all_cores": round(threads * per * D / ta, 1), "cores": threads,
+            "sample": f"{per} seeds x 1M-dim on 1 core, {threads * per} on {threads} threads; median of {n1}/{na} "
+                      "runs; oracle/sda_oracle.c at -O2"}
 
 
 class TimedEngine:
@@ -154,6 +227,9 @@ class TimedEngine:
     def combine_accumulate_dev(self, *a):
         self._timed(self.eng.combine_accumulate_dev, *a)
 
+    def combine_split_dev(self, *a):            # pass 1 of the participation split (N > 1)
+        self._timed(self.eng.combine_split_dev, *a)
+
 
 def exact_sample_check(torch, shares, cols, m, got, reps=1, rows=None):
     """Bit-exact check of combiner.rs:22-25 on sampled columns: the sequential recurrence
@@ -169,20 +245,65 @@ def exact_sample_check(torch, shares, cols, m, got, reps=1, rows=None):
     return bool((r == got[cols].cpu().numpy()).all())
 
 
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` (N > 1) started without a launcher: start N ranks of this same command, one per GPU
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets them), wait for all of them
+    and return the first failing exit code (0 if all passed).  Rank 0 prints the JSON line to the
+    inherited stdout.  Runs before this process touches the GPU (only the device COUNT is read, which
+    does not initialise it), so the ranks own their devices."""
+    import signal
+    import socket
+    import subprocess
+    if os.environ.get("SDA_DIST_BACKEND", "nccl") == "nccl":
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            log(f"bench.py: --gpus {n} needs {n} GPUs, {have} visible (SDA_DIST_BACKEND=gloo rehearses "
+                f"N ranks on fewer devices)")
+            return 2
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks")
+                for q in alive:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch with --nproc-per-node equal to --gpus")
+        sys.exit(2)
+
     import torch
     import torch.distributed as dist
 
     from sda_amd import Engine, schemes as S
     from sda_amd import distributed as Dd
     from sda_amd import engine as E
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     # one rank per GPU; SDA_DIST_BACKEND=gloo rehearses N ranks on fewer devices (RCCL refuses two
     # ranks on one device): ranks then share GPUs round-robin, and the collectives run over gloo
     backend = os.environ.get("SDA_DIST_BACKEND", "nccl")
@@ -270,9 +391,10 @@ def main():
         if not ok:
             raise SystemExit("combine result check FAILED")
         rows_per_launch = tile if tile else N
-        # one launch reads its rows and writes D results; an accumulating tile launch also reads the
-        # running partial (16 D).  `value` counts the job's own bytes only: N x D shares in, D out.
-        bytes_per_launch = 8.0 * rows_per_launch * D + (16.0 if tile else 8.0) * D
+        # one launch reads its rows and writes D results; an accumulating launch (row tiles, and the
+        # participation split's pass 1 at N > 1) also reads the running partial (16 D).  `value` counts
+        # the job's own bytes only: N x D shares in, D out.
+        bytes_per_launch = 8.0 * rows_per_launch * D + (16.0 if (tile or world > 1) else 8.0) * D
         total_bytes = (8.0 * N * D + 8.0 * D) * args.steps * world
         value = total_bytes / dt / 1e9
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
@@ -296,6 +418,44 @@ def main():
                 "roofline_frac": bytes_per_launch / (s_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                 "check": "bit-exact on 4096 sampled columns (sequential recurrence replayed on the host)"}
             log(f"[combine_signed] {json.dumps(side['combine_signed'])}")
+        if not args.no_signed_split and world > 1 and not tile:
+            # the same signed worst case through the participation split at N > 1: the exact two-pass
+            # path (pass 1 + flags, all-gather, replay of the sign events, MAX-resolve)
+            eng.synth_fill_dev(shares.data_ptr(), N, D, SEED_BASE + 12 + 1000 * rank, -(m - 1), m, stream())
+            sst = Dd.SplitStats()
+            sstep = lambda: Dd.combine_rows_sharded(eng, m, shares.data_ptr(), N, D, D, partial, out, stats=sst)  # noqa
+            sstep()
+            torch.cuda.synchronize()
+            barrier()
+            reps = max(3, args.steps // 4)
+            ts = time.perf_counter()
+            for _ in range(reps):
+                sstep()
+            torch.cuda.synchronize()
+            barrier()
+            tt = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            s_dt = float(tt.item()) / reps
+            ok = True
+            if not args.no_check:     # replay the reference recurrence over all ranks' rows, in rank order
+                c256 = cols[:256]
+                mine = shares[:, c256].contiguous()
+                allr = [torch.empty_like(mine) for _ in range(world)]
+                dist.all_gather(allr, mine)
+                r = np.zeros(256, dtype=np.int64)
+                for blk in allr:
+                    for row in blk.cpu().numpy():
+                        r = np.fmod(r + row, m)
+                ok = bool((r == out[c256].cpu().numpy()).all()) and sst.signed
+            if not ok:
+                raise SystemExit("signed participation split check FAILED")
+            side["combine_signed_split"] = {
+                "config": f"configs[1] with uniform (-m, m) shares on each of {world} ranks: exact participation "
+                          "split of a signed job (two passes over the rows, all-gather + MAX all-reduce)",
+                "ms_per_step": s_dt * 1e3, "GBps_all_gpus": 8.0 * (N * D + D) * world / s_dt / 1e9,
+                "passes": sst.passes,
+                "check": "bit-exact on 256 sampled columns: the reference recurrence over all ranks' rows in order"}
+            log(f"[combine_signed_split] {json.dumps(side['combine_signed_split'])}")
         del shares
 
     # ---------------- side legs (rank-local, reported by rank 0) ----------------

@@ -168,11 +168,36 @@ sda_status sda_combine_accumulate_dev(sda_engine* h, int64_t modulus, const int6
                                       uint64_t n, uint64_t dim, uint64_t row_stride,
                                       int64_t* inout, void* stream);
 
-/* Multi-GPU finalize: `sums` are the two's-complement u64 sums (RCCL-reduced) of per-GPU
- * combine results; out = canonical residue in [0, m).  Exact w.r.t. the reference when all
- * combined inputs were non-negative (DESIGN.md "multi-GPU"). */
+/* Multi-GPU finalize: `sums` are the int64 sums (RCCL-reduced; |sum| <= 2^63 - 1, signed allowed)
+ * of per-GPU combine results; out = their canonical residue in [0, m).  Exact w.r.t. the reference
+ * when all combined inputs were non-negative. */
 sda_status sda_combine_finalize_dev(sda_engine* h, int64_t modulus, const int64_t* sums,
                                     uint64_t dim, int64_t* out, void* stream);
+
+/* ---- participation split of the clerk combine over G ranks ----
+ * The reference's result (combiner.rs:16-28) is order dependent when inputs are negative (Additive
+ * last shares are signed, additive.rs:46), so rank g (rows of participations g's contiguous range):
+ *  1. sda_combine_split_dev: the exact recurrence continued from inout (zeros before the first row
+ *     tile), which also sets flags[0] = 1 if an input is < 0 and flags[1] = 1 if an input lies outside
+ *     [-(2^63 - m), 2^63 - m] (the reference's `r + v` may wrap there: no split reproduces that, refuse
+ *     the split).  flags: device int64[2], zeroed by the caller, only ever set to 1.
+ *  2. no rank flagged a negative input: all-reduce(SUM) the G results, sda_combine_finalize_dev.
+ *  3. otherwise: all-gather the G results into gathered[G][dim]; sda_combine_split_prefix_dev gives
+ *     c_in (canonical sum of ranks < g), total (canonical sum of all) and the initial code;
+ *     sda_combine_split_replay_dev replays this rank's row tiles from c_in (state in/out) recording the
+ *     last sign event in code (0 none, 2g+1 reset, 2g+2 set); all-reduce(MAX) the codes over the ranks;
+ *     sda_combine_split_resolve_dev writes the reference's signed result. */
+sda_status sda_combine_split_dev(sda_engine* h, int64_t modulus, const int64_t* shares, uint64_t n,
+                                 uint64_t dim, uint64_t row_stride, int64_t* inout, int64_t* flags,
+                                 void* stream);
+sda_status sda_combine_split_prefix_dev(sda_engine* h, int64_t modulus, const int64_t* gathered,
+                                        uint64_t world, uint64_t rank, uint64_t dim, int64_t* c_in,
+                                        int64_t* total, int32_t* code, void* stream);
+sda_status sda_combine_split_replay_dev(sda_engine* h, int64_t modulus, const int64_t* shares, uint64_t n,
+                                        uint64_t dim, uint64_t row_stride, uint64_t rank, int64_t* state,
+                                        int32_t* code, void* stream);
+sda_status sda_combine_split_resolve_dev(sda_engine* h, int64_t modulus, const int64_t* total,
+                                         const int32_t* code, uint64_t dim, int64_t* out, void* stream);
 
 /* Packed-Shamir share generation for `n_vectors` participant vectors at once:
  * secrets [n_vectors][dimension], draws [n_vectors][B][t], out [n_vectors][n][B]. */

@@ -20,6 +20,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <atomic>
+
 #include "kernels.h"
 
 namespace sda {
@@ -414,10 +416,14 @@ static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_
     // Seeds split over grid.y chunks until the grid holds one full round of resident workgroups (the
     // kernel is VALU-bound: more chunks only add atomic merges -- A/B in profiles/r02/ab_chacha.txt).
     // The u64 accumulators receive one canonical partial (< m) per chunk (headroom).
-    static int cap_wgs = 0;
+    // cached per device (a process may drive devices of different sizes); a racing first call computes
+    // the same value twice, and the relaxed atomic makes that benign
+    static std::atomic<int> cap_cache[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int cap_wgs = (dev >= 0 && dev < 64) ? cap_cache[dev].load(std::memory_order_relaxed) : 0;
     if (cap_wgs == 0) {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
+        int cus = 0, per_cu = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chacha_combine_kernel<true, false>, 256, 0);
         // the API can be one block per CU high at 81-96 SGPRs (MI355X_MICROARCH.md): also bound it by
@@ -429,6 +435,7 @@ static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_
             if (by_vgpr < per_cu) per_cu = by_vgpr;
         }
         cap_wgs = (cus > 0 && per_cu > 0) ? cus * per_cu : 2048;
+        if (dev >= 0 && dev < 64) cap_cache[dev].store(cap_wgs, std::memory_order_relaxed);
     }
     uint64_t max_c = n_seeds ? n_seeds : 1;
     if (max_c > 65535) max_c = 65535;

@@ -32,11 +32,17 @@ __device__ __forceinline__ int64_t lane_of(const typename vec_t<T, VEC>::type& v
 // a clerk job streamed through HBM in row tiles is bit-identical to one pass over all rows.
 // T: the row element type -- int64_t (the ABI's shares), or int32_t for decoded field shares
 // (the clerk's decode -> combine, whose payload values fit: half the bytes to read).
-template <typename T, int VEC, int UNROLL, bool SMALL_M, bool ACC>
+// FLAG (pass 1 of the multi-GPU participation split): also raise flags[0] when an input
+// is negative (the ranks' canonical sums then lose the sign the reference's order gives: the split
+// runs its replay pass) and flags[1] when an input lies outside [-(2^63 - m), 2^63 - m] (the
+// reference's `r + v` may wrap i64 there, which no split can reproduce).  One OR of the high word per
+// element (plus a 64-bit range check); every writer stores the same 1, so plain stores suffice.
+template <typename T, int VEC, int UNROLL, bool SMALL_M, bool ACC, bool FLAG = false>
 __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict__ in,
                                                             uint64_t n, uint64_t n_lanes,
                                                             uint64_t stride,
-                                                            int64_t* __restrict__ out, Mod64 M) {
+                                                            int64_t* __restrict__ out, Mod64 M,
+                                                            int64_t* __restrict__ flags = nullptr) {
     typedef typename vec_t<T, VEC>::type V;
     const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= n_lanes) return;
@@ -46,6 +52,15 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict_
 #pragma unroll
     for (int e = 0; e < VEC; ++e) r[e] = ACC ? out[lane * VEC + e] : 0;
 
+    uint32_t neg = 0, risk = 0;
+    const uint64_t lim = ((uint64_t)1 << 63) - M.m;        // no-wrap range [-lim, lim]
+    auto step = [&](int e, int64_t x) {
+        r[e] = add_trem(r[e], x, M, SMALL_M);
+        if constexpr (FLAG) {
+            neg |= hi32(x);
+            risk |= (uint32_t)((uint64_t)x + lim > 2 * lim);
+        }
+    };
     uint64_t i = 0;
     for (; i + UNROLL <= n; i += UNROLL) {
         V v[UNROLL];
@@ -55,13 +70,17 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict_
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) r[e] = add_trem(r[e], lane_of<T, VEC>(v[u], e), M, SMALL_M);
+            for (int e = 0; e < VEC; ++e) step(e, lane_of<T, VEC>(v[u], e));
     }
     for (; i < n; ++i) {
         V v = __builtin_nontemporal_load(p);
         p += vstride;
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) r[e] = add_trem(r[e], lane_of<T, VEC>(v, e), M, SMALL_M);
+        for (int e = 0; e < VEC; ++e) step(e, lane_of<T, VEC>(v, e));
+    }
+    if constexpr (FLAG) {
+        if ((int32_t)neg < 0) flags[0] = 1;
+        if (risk) flags[1] = 1;
     }
     typedef typename vec_t<int64_t, VEC>::type VO;
     VO o;
@@ -72,24 +91,136 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict_
     reinterpret_cast<VO*>(out)[lane] = o;
 }
 
-template <typename T, int VEC, int UNROLL, bool ACC>
+template <typename T, int VEC, int UNROLL, bool ACC, bool FLAG = false>
 hipError_t launch_vec(const T* in, uint64_t n, uint64_t dim, uint64_t stride, int64_t* out,
-                      const Mod64& M, bool small_m, hipStream_t s) {
+                      const Mod64& M, bool small_m, hipStream_t s, int64_t* flags = nullptr) {
     const uint64_t n_lanes = dim / VEC;
     const uint64_t blocks = (n_lanes + 255) / 256;
     if (small_m)
-        hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, true, ACC>), dim3((unsigned)blocks), dim3(256), 0, s,
-                           in, n, n_lanes, stride, out, M);
+        hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, true, ACC, FLAG>), dim3((unsigned)blocks), dim3(256),
+                           0, s, in, n, n_lanes, stride, out, M, flags);
     else
-        hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, false, ACC>), dim3((unsigned)blocks), dim3(256), 0, s,
-                           in, n, n_lanes, stride, out, M);
+        hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, false, ACC, FLAG>), dim3((unsigned)blocks), dim3(256),
+                           0, s, in, n, n_lanes, stride, out, M, flags);
     return hipGetLastError();
 }
 
+// canonical residue in [0, m) of a signed i64 value
+__device__ __forceinline__ int64_t canon64(int64_t v, const Mod64& M) {
+    const int64_t r = trem64(v, M);
+    return r < 0 ? r + (int64_t)M.m : r;
+}
+
+// Multi-GPU finalize: the all-reduced int64 sums of the ranks' results (|sum| <= G (m - 1) <= 2^63 - 1,
+// checked on the host), signed when the ranks' results were -> their canonical residue.
 __global__ __launch_bounds__(256) void mod_canonical_kernel(const int64_t* __restrict__ sums, uint64_t dim,
                                                             int64_t* __restrict__ out, Mod64 M) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < dim) out[i] = (int64_t)umod64((uint64_t)sums[i], M);
+    if (i < dim) out[i] = canon64(sums[i], M);
+}
+
+// ---- signed participation split, pass 2 (DESIGN.md §5 "signed inputs") ----
+// Keep the reference's running value as r = c - m s: c its canonical residue, s = [r < 0] (s = 1 needs
+// c != 0).  One step r' = (r + v) % m (no i64 wrap: pass 1 refused such v) gives c' = (c + v) mod m and
+//   v >= 0:  s' = s AND [c + v < m]                  -> "reset" when c + v >= m, else no event
+//   v <  0:  s' = (s OR [c + v < 0]) AND [c' != 0]   -> "reset" when c' = 0, "set" when c + v < 0,
+//                                                       else no event
+// so, given c at the chunk's start, every step maps s to s, to 0 or to 1, and a chunk of rows maps it
+// through its LAST event.  The chunk's c trajectory needs only the incoming residue c_in (the other
+// ranks' pass-1 sums), never s: this pass replays it and records the last event as a code that an
+// all-reduce MAX over the ranks resolves in participation order -- 0 none, 2g+1 reset, 2g+2 set (g = the
+// rank).  A step with c' = 0 always leaves s' = 0, so it may be called a reset whatever the sign of v.
+template <int VEC, int UNROLL, bool SMALL_M>
+__global__ __launch_bounds__(256) void combine_replay_kernel(const int64_t* __restrict__ in, uint64_t n,
+                                                             uint64_t n_lanes, uint64_t stride,
+                                                             int64_t* __restrict__ state, int32_t* __restrict__ code,
+                                                             int32_t reset_code, Mod64 M) {
+    typedef typename vec_t<int64_t, VEC>::type V;
+    const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= n_lanes) return;
+    const V* p = reinterpret_cast<const V*>(in + lane * VEC);
+    const uint64_t vstride = stride / VEC;
+    const int64_t m = (int64_t)M.m;
+    int64_t c[VEC];
+    int32_t cd[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+        c[e] = state[lane * VEC + e];
+        cd[e] = code[lane * VEC + e];
+    }
+    auto step = [&](int e, int64_t v) {
+        int64_t cn;
+        bool hi, lo;
+        if (SMALL_M && ((uint64_t)v + (uint64_t)(m - 1) < (uint64_t)(2 * m - 1))) {   // v in (-m, m)
+            const int64_t t = c[e] + v;                  // (-m, 2m)
+            hi = t >= m;
+            lo = t < 0;
+            cn = hi ? t - m : (lo ? t + m : t);
+        } else {                                         // any v, any m: exact unsigned forms
+            const uint64_t uc = (uint64_t)c[e];
+            const uint64_t mag = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+            const uint64_t rr = umod64(mag, M);
+            const uint64_t vr = (v < 0 && rr) ? M.m - rr : rr;              // v mod m, canonical
+            const uint64_t sum = uc + vr;                                   // < 2m < 2^64
+            cn = (int64_t)(sum >= M.m ? sum - M.m : sum);
+            hi = v >= 0 && mag >= M.m - uc;              // c + v >= m
+            lo = v < 0 && mag > uc;                      // c + v < 0
+        }
+        c[e] = cn;
+        cd[e] = (cn == 0 || hi) ? reset_code : (lo ? reset_code + 1 : cd[e]);
+    };
+    uint64_t i = 0;
+    for (; i + UNROLL <= n; i += UNROLL) {
+        V v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) v[u] = __builtin_nontemporal_load(p + (uint64_t)u * vstride);
+        p += (uint64_t)UNROLL * vstride;
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) step(e, lane_of<int64_t, VEC>(v[u], e));
+    }
+    for (; i < n; ++i) {
+        V v = __builtin_nontemporal_load(p);
+        p += vstride;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) step(e, lane_of<int64_t, VEC>(v, e));
+    }
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+        state[lane * VEC + e] = c[e];
+        code[lane * VEC + e] = cd[e];
+    }
+}
+
+// gathered [world][dim] = every rank's pass-1 result: c_in = canonical(sum over ranks < rank),
+// total = canonical(sum over all ranks); code = rank 0's own sign (its pass 1 started at the job's
+// start, r = 0): 1 + [r_0 < 0], else 0 (no event yet).  |partial sums| <= world (m - 1) <= 2^63 - 1.
+__global__ __launch_bounds__(256) void split_prefix_kernel(const int64_t* __restrict__ gathered, uint64_t world,
+                                                           uint64_t rank, uint64_t dim, int64_t* __restrict__ c_in,
+                                                           int64_t* __restrict__ total, int32_t* __restrict__ code,
+                                                           Mod64 M) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= dim) return;
+    int64_t before = 0, all = 0;
+    for (uint64_t g = 0; g < world; ++g) {
+        const int64_t v = gathered[g * dim + i];
+        if (g < rank) before += v;
+        all += v;
+    }
+    c_in[i] = canon64(before, M);
+    total[i] = canon64(all, M);
+    code[i] = rank == 0 ? 1 + (gathered[i] < 0) : 0;
+}
+
+// out = the reference's signed result: total - m when the last sign event (MAX-reduced code) set s.
+__global__ __launch_bounds__(256) void split_resolve_kernel(const int64_t* __restrict__ total,
+                                                            const int32_t* __restrict__ code, uint64_t dim,
+                                                            int64_t* __restrict__ out, int64_t m) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= dim) return;
+    const bool neg = ((code[i] - 1) & 1) != 0;
+    out[i] = total[i] - (neg ? m : 0);
 }
 
 }  // namespace
@@ -107,6 +238,53 @@ hipError_t launch_combine_exact(const int64_t* in, uint64_t n, uint64_t dim, uin
                   : launch_vec<int64_t, 1, 8, true>(in, n, dim, stride, out, M, small_m, s);
     return v2 ? launch_vec<int64_t, 2, 8, false>(in, n, dim, stride, out, M, small_m, s)
               : launch_vec<int64_t, 1, 8, false>(in, n, dim, stride, out, M, small_m, s);
+}
+
+hipError_t launch_combine_split(const int64_t* in, uint64_t n, uint64_t dim, uint64_t stride, int64_t* inout,
+                                int64_t modulus, int64_t* flags, hipStream_t s) {
+    if (dim == 0 || n == 0) return hipSuccess;
+    const Mod64 M = make_mod64(modulus);
+    const bool small_m = modulus <= ((int64_t)1 << 62);
+    const uintptr_t a = (uintptr_t)in | (uintptr_t)inout;
+    const bool v2 = dim % 2 == 0 && stride % 2 == 0 && (a % 16) == 0;
+    return v2 ? launch_vec<int64_t, 2, 8, true, true>(in, n, dim, stride, inout, M, small_m, s, flags)
+              : launch_vec<int64_t, 1, 8, true, true>(in, n, dim, stride, inout, M, small_m, s, flags);
+}
+
+hipError_t launch_combine_replay(const int64_t* in, uint64_t n, uint64_t dim, uint64_t stride, int64_t* state,
+                                 int32_t* code, int32_t reset_code, int64_t modulus, hipStream_t s) {
+    if (dim == 0 || n == 0) return hipSuccess;
+    const Mod64 M = make_mod64(modulus);
+    const bool small_m = modulus <= ((int64_t)1 << 62);
+    const uintptr_t a = (uintptr_t)in | (uintptr_t)state;
+    const bool v2 = dim % 2 == 0 && stride % 2 == 0 && (a % 16) == 0 && (uintptr_t)code % 8 == 0;
+    const int vec = v2 ? 2 : 1;
+    const uint64_t n_lanes = dim / vec;
+    const dim3 grid((unsigned)((n_lanes + 255) / 256));
+    if (v2) {
+        if (small_m) hipLaunchKernelGGL((combine_replay_kernel<2, 8, true>), grid, dim3(256), 0, s, in, n, n_lanes, stride, state, code, reset_code, M);
+        else hipLaunchKernelGGL((combine_replay_kernel<2, 8, false>), grid, dim3(256), 0, s, in, n, n_lanes, stride, state, code, reset_code, M);
+    } else {
+        if (small_m) hipLaunchKernelGGL((combine_replay_kernel<1, 8, true>), grid, dim3(256), 0, s, in, n, n_lanes, stride, state, code, reset_code, M);
+        else hipLaunchKernelGGL((combine_replay_kernel<1, 8, false>), grid, dim3(256), 0, s, in, n, n_lanes, stride, state, code, reset_code, M);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_split_prefix(const int64_t* gathered, uint64_t world, uint64_t rank, uint64_t dim, int64_t* c_in,
+                               int64_t* total, int32_t* code, int64_t modulus, hipStream_t s) {
+    if (dim == 0) return hipSuccess;
+    hipLaunchKernelGGL(split_prefix_kernel, dim3((unsigned)((dim + 255) / 256)), dim3(256), 0, s, gathered, world,
+                       rank, dim, c_in, total, code, make_mod64(modulus));
+    return hipGetLastError();
+}
+
+hipError_t launch_split_resolve(const int64_t* total, const int32_t* code, uint64_t dim, int64_t* out,
+                                int64_t modulus, hipStream_t s) {
+    if (dim == 0) return hipSuccess;
+    hipLaunchKernelGGL(split_resolve_kernel, dim3((unsigned)((dim + 255) / 256)), dim3(256), 0, s, total, code, dim,
+                       out, modulus);
+    return hipGetLastError();
 }
 
 hipError_t launch_combine_exact32(const int32_t* in, uint64_t n, uint64_t dim, uint64_t stride,

@@ -47,7 +47,21 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// The handle and stream of the call in progress on this thread (set by pick()): when the call returns,
+// its stream records the handle's order event, so the NEXT call -- on whatever stream -- only waits on
+// that event and never touches this call's stream again (the caller may destroy it in between).
+thread_local sda_engine* t_call_h = nullptr;
+thread_local hipStream_t t_call_s = nullptr;
+
+void end_call() {
+    if (t_call_h) {
+        (void)hipEventRecord(t_call_h->order_ev, t_call_s);
+        t_call_h = nullptr;
+    }
+}
+
 sda_status fail(sda_status st, const char* fmt, ...) {
+    end_call();
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -58,6 +72,7 @@ sda_status fail(sda_status st, const char* fmt, ...) {
 }
 
 sda_status ok() {
+    end_call();
     g_last_error.clear();
     return SDA_OK;
 }
@@ -83,16 +98,19 @@ sda_status ensure(void** buf, size_t* have, size_t need) {
 
 // `_dev` entry points run on the caller's stream; NULL is the HIP null (default) stream, which is
 // also what torch's default stream reports -- so work stays ordered with the caller's own ops.
-// Switching streams orders the new stream after the previous one (event wait, no host sync), so a
-// call never reuses a scratch buffer that work queued on another stream may still be reading.
+// Switching streams orders the new stream after the previous call (event wait, no host sync), so a
+// call never reuses a scratch buffer that work queued on another stream may still be reading.  The
+// event was recorded on the previous call's stream when that call returned (end_call), so the previous
+// stream itself is never touched here and may have been destroyed since.
 hipStream_t pick(sda_engine* h, void* stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (s != h->last_stream) {
-        if (hipEventRecord(h->order_ev, h->last_stream) != hipSuccess ||
-            hipStreamWaitEvent(s, h->order_ev, 0) != hipSuccess)
-            (void)hipStreamSynchronize(h->last_stream);      // same ordering, from the host
+        if (hipStreamWaitEvent(s, h->order_ev, 0) != hipSuccess)
+            (void)hipEventSynchronize(h->order_ev);          // same ordering, from the host
         h->last_stream = s;
     }
+    t_call_h = h;
+    t_call_s = s;
     return s;
 }
 
@@ -251,6 +269,7 @@ sda_status sda_engine_create(int device_ordinal, sda_engine** out) {
 
 void sda_engine_destroy(sda_engine* h) {
     if (!h) return;
+    if (t_call_h == h) t_call_h = nullptr;
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();            // _dev work may still be queued on callers' streams
     if (h->work) (void)hipFree(h->work);
@@ -407,7 +426,7 @@ sda_status sda_secret_reconstruct(sda_engine* h, const sda_sharing_scheme* s, ui
     for (uint64_t i = 0; i < n_rows; ++i)
         if (lens[i] < (enough ? B : 1))
             return fail(SDA_ERR_PRECONDITION, "index out of bounds: row %llu has %llu < %llu batches",
-                        (unsigned long long)i, (unsigned long long)lens[i], (unsigned long long)B);
+                        (unsigned long long)i, (unsigned long long)lens[i], (unsigned long long)(enough ? B : 1));
     if (!enough)
         return fail(SDA_ERR_NOT_ENOUGH_SHARES, "Not enough shares to reconstruct (%llu < %llu)",
                     (unsigned long long)n_rows, (unsigned long long)(s->privacy_threshold + k));
@@ -603,6 +622,56 @@ sda_status sda_combine_finalize_dev(sda_engine* h, int64_t modulus, const int64_
     if (sda_status st = modulus_abs(modulus, &m)) return st;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(sda::launch_mod_canonical(sums, dim, out, m, pick(h, stream)));
+    return ok();
+}
+
+sda_status sda_combine_split_dev(sda_engine* h, int64_t modulus, const int64_t* shares, uint64_t n, uint64_t dim,
+                                 uint64_t row_stride, int64_t* inout, int64_t* flags, void* stream) {
+    if (!h || (dim && (!inout || !flags || (n && !shares)))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (n > 1 && row_stride < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "row_stride < dim");
+    int64_t m;
+    if (sda_status st = modulus_abs(modulus, &m)) return st;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(sda::launch_combine_split(shares, n, dim, n > 1 ? row_stride : dim, inout, m, flags, pick(h, stream)));
+    return ok();
+}
+
+sda_status sda_combine_split_prefix_dev(sda_engine* h, int64_t modulus, const int64_t* gathered, uint64_t world,
+                                        uint64_t rank, uint64_t dim, int64_t* c_in, int64_t* total, int32_t* code,
+                                        void* stream) {
+    if (!h || (dim && (!gathered || !c_in || !total || !code))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (rank >= world || world > (1u << 29)) return fail(SDA_ERR_INVALID_ARGUMENT, "rank %llu of world %llu",
+                                                         (unsigned long long)rank, (unsigned long long)world);
+    int64_t m;
+    if (sda_status st = modulus_abs(modulus, &m)) return st;
+    if ((unsigned __int128)world * (uint64_t)(m - 1) > (unsigned __int128)INT64_MAX)
+        return fail(SDA_ERR_INVALID_ARGUMENT, "world * (m - 1) exceeds 2^63 - 1");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(sda::launch_split_prefix(gathered, world, rank, dim, c_in, total, code, m, pick(h, stream)));
+    return ok();
+}
+
+sda_status sda_combine_split_replay_dev(sda_engine* h, int64_t modulus, const int64_t* shares, uint64_t n,
+                                        uint64_t dim, uint64_t row_stride, uint64_t rank, int64_t* state,
+                                        int32_t* code, void* stream) {
+    if (!h || (dim && (!state || !code || (n && !shares)))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (n > 1 && row_stride < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "row_stride < dim");
+    if (rank > (1u << 29)) return fail(SDA_ERR_INVALID_ARGUMENT, "rank %llu too large", (unsigned long long)rank);
+    int64_t m;
+    if (sda_status st = modulus_abs(modulus, &m)) return st;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(sda::launch_combine_replay(shares, n, dim, n > 1 ? row_stride : dim, state, code, (int32_t)(2 * rank + 1),
+                                       m, pick(h, stream)));
+    return ok();
+}
+
+sda_status sda_combine_split_resolve_dev(sda_engine* h, int64_t modulus, const int64_t* total, const int32_t* code,
+                                         uint64_t dim, int64_t* out, void* stream) {
+    if (!h || (dim && (!total || !code || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
+    int64_t m;
+    if (sda_status st = modulus_abs(modulus, &m)) return st;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(sda::launch_split_resolve(total, code, dim, out, m, pick(h, stream)));
     return ok();
 }
 

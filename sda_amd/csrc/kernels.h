@@ -18,9 +18,21 @@ hipError_t launch_combine_exact(const int64_t* in, uint64_t n, uint64_t dim, uin
 // The same recurrence over int32 rows (decoded field shares: the clerk's decode -> combine).
 hipError_t launch_combine_exact32(const int32_t* in, uint64_t n, uint64_t dim, uint64_t stride,
                                   int64_t* out, int64_t modulus, hipStream_t s);
-// Canonical residue of u64 sums (multi-GPU finalize).
+// Canonical residue of the int64 sums of the ranks' results (multi-GPU finalize; signed sums allowed).
 hipError_t launch_mod_canonical(const int64_t* sums, uint64_t dim, int64_t* out, int64_t modulus,
                                 hipStream_t s);
+// Participation split.  Pass 1: the exact recurrence continued from inout that also sets
+// flags[0] = 1 (an input < 0) / flags[1] = 1 (an input outside [-(2^63 - m), 2^63 - m]).
+hipError_t launch_combine_split(const int64_t* in, uint64_t n, uint64_t dim, uint64_t stride, int64_t* inout,
+                                int64_t modulus, int64_t* flags, hipStream_t s);
+// Pass 2 (signed inputs): replay the canonical trajectory from state (c_in), recording the last sign
+// event in code (reset_code = 2 rank + 1 on a reset, + 1 on a set; unchanged without an event).
+hipError_t launch_combine_replay(const int64_t* in, uint64_t n, uint64_t dim, uint64_t stride, int64_t* state,
+                                 int32_t* code, int32_t reset_code, int64_t modulus, hipStream_t s);
+hipError_t launch_split_prefix(const int64_t* gathered, uint64_t world, uint64_t rank, uint64_t dim, int64_t* c_in,
+                               int64_t* total, int32_t* code, int64_t modulus, hipStream_t s);
+hipError_t launch_split_resolve(const int64_t* total, const int32_t* code, uint64_t dim, int64_t* out,
+                                int64_t modulus, hipStream_t s);
 
 // ---- elementwise.hip ----
 hipError_t launch_additive_generate(const int64_t* secrets, uint64_t D, const int64_t* draws,
@@ -45,6 +57,7 @@ struct DeviceTable {
     size_t cap = 0;
     void* ws = nullptr;           // packed_wide.hip: per-lane transform workspace (grows, never shrinks)
     size_t ws_cap = 0;
+    uint32_t flags = 0;           // per-table launch choices (packed_gen.hip: bit 0 = sign-bit kernel)
 };
 hipError_t ensure_table(DeviceTable& t, const std::vector<uint8_t>& key, const void* host, size_t bytes);
 void free_table(DeviceTable& t);
@@ -54,6 +67,7 @@ struct PackedGenArgs {
     const int64_t* draws; int64_t* out;
     bool canonical = false;       // shares as canonical residues in [0, p) instead of tss' signed values
     uint32_t prime = 0;           // set by launch_packed_generate (selects the lazy-truncation kernel)
+    bool signbit = false;         // set by launch_packed_generate (sign-bit radix-2 half, packed_gen.hip)
 };
 // Exact share-gen uses lazy truncation (packed_gen.hip: Trunc<true>) for primes at least this big.
 constexpr uint32_t kLazyTruncMinP = 1u << 24;

@@ -71,6 +71,10 @@ struct GenTables {
     uint32_t tw2[64], tw2_m[64];    // radix-2 level len: entries [len/2 - 1, len - 1)
     uint32_t tw3[120], tw3_m[120];  // radix-3 level len: entries [(len-3)/2, (len-3)/2 + len)
     uint32_t sq3[120], sq3_m[120];  // x^2 % p per radix-3 entry
+    // Sign-bit share-gen (packed_gen.hip, SIGNBIT): (u + w c) % p has the sign of c whenever |w c| >= p,
+    // i.e. |c| >= ceil(p / w); big2 = the largest such bound over the non-unit radix-2 twiddles, big3 over
+    // the radix-3 twiddles of the first radix-3 level (its groups are b + x c: d is zero padding).
+    uint32_t big2, big3;
 };
 
 inline GenTables make_gen_tables(uint32_t L, uint32_t N3, int64_t p, int64_t ws, int64_t wn) {
@@ -94,6 +98,9 @@ inline GenTables make_gen_tables(uint32_t L, uint32_t N3, int64_t p, int64_t ws,
             }
         }
     }
+    T.big2 = 1;
+    for (uint32_t e = 1; e < L - 1; ++e)
+        if (T.tw2[e] > 1) { const uint64_t b = ((uint64_t)p + T.tw2[e] - 1) / T.tw2[e]; if (b > T.big2) T.big2 = (uint32_t)b; }
     {
         int64_t om = wn;
         std::vector<int64_t> per_level;
@@ -108,6 +115,11 @@ inline GenTables make_gen_tables(uint32_t L, uint32_t N3, int64_t p, int64_t ws,
                 T.sq3[o] = (uint32_t)x2; T.sq3_m[o] = to_mont(x2, p);
             }
         }
+    }
+    T.big3 = 1;
+    for (uint32_t j = 1; j < 3 && j < N3; ++j) {          // first radix-3 level: entries 1, 2 (len 3)
+        const uint64_t b = ((uint64_t)p + T.tw3[j] - 1) / T.tw3[j];
+        if (b > T.big3) T.big3 = (uint32_t)b;
     }
     return T;
 }

@@ -1,4 +1,6 @@
 // packed_gen.hip -- packed-Shamir share generation (see packed_common.h for the algorithm).
+#include <stdlib.h>
+
 #include "packed_common.h"
 
 namespace sda {
@@ -43,6 +45,40 @@ __device__ __forceinline__ void bfly2_unit(FE& u, FE& c, uint32_t p, TR& tr) {
     c = FE{tr(c2, (uint32_t)s2, p), c2};
     tr.note2(u.s, c.s);
 }
+
+// SIGNBIT (lazy exact kernel): the radix-2 half of the transform on (residue c, sign word n) pairs,
+// value = c - p [n < 0] -- the reveal's sign-bit formulation carried to share-gen:
+//   unit butterfly   (u + c) % p: sign MAJ(n_u, n_c, [c_u + c_c < p]);  (u - c) % p: MAJ(n_u, ~n_c, [c_u < c_c])
+//   twiddle w != 1   (u +- w c) % p: the exact product dominates |u| < p whenever |w c| >= p, so the
+//                    signs are n_c and ~n_c -- no 64-bit sign products, no truncation ops;
+//   x * len_inv % p  keeps the sign of x (len_inv > 0).
+// Exact unless a butterfly output's residue is 0 (it might then carry the sign of a nonzero multiple of
+// p, which tss truncates to 0) or a multiplied operand is small, |c| < ceil(p / w).  RangeTrap keeps a
+// running min of the output residues and a running max of the shifted multiplied ones (two values per
+// v_min3 / v_max3); such batches (probability ~ 1/p per output, ~ 2 big2 / p per product: ~1e-8 at
+// configs[2]) go to the generic fix-up kernel like the lazy truncation's -p trap.
+struct RangeTrap {
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    uint32_t lpend = 0, hpend = 0;
+    bool lhas = false, hhas = false;      // constant at every point of the unrolled code
+    __device__ __forceinline__ void lo2(uint32_t a, uint32_t b) { asm("v_min3_u32 %0, %0, %1, %2" : "+v"(lo) : "v"(a), "v"(b)); }
+    __device__ __forceinline__ void hi2(uint32_t a, uint32_t b) { asm("v_max3_u32 %0, %0, %1, %2" : "+v"(hi) : "v"(a), "v"(b)); }
+    // a butterfly output's residue: 0 is the trap (0 with the sign set would be a nonzero multiple of p)
+    __device__ __forceinline__ void out1(uint32_t c) {
+        if (lhas) { lo2(lpend, c); lhas = false; } else { lpend = c; lhas = true; }
+    }
+    // a multiplied operand's residue c must lie in [big, p - big]: c - big (wrapping below big) <= p - 2 big
+    __device__ __forceinline__ void mul1(uint32_t c, uint32_t big) {
+        const uint32_t x = c - big;
+        if (hhas) { hi2(hpend, x); hhas = false; } else { hpend = x; hhas = true; }
+    }
+    __device__ __forceinline__ bool bad(uint32_t big, uint32_t p) {
+        if (lhas) lo2(lpend, lpend);
+        if (hhas) hi2(hpend, hpend);
+        lhas = hhas = false;
+        return lo == 0 || hi > p - 2 * big;
+    }
+};
 
 // Compile-time map of the radix-3 registers that hold a known zero (the zero padding of
 // coefficients L..N3-1) after `stage` levels: a group whose c and d are zero just copies b.
@@ -160,7 +196,7 @@ __device__ __forceinline__ void transform_canon(const int64_t (&raw)[L], const G
 // per row pair (13 dwordx4 instead of 26 dwordx2 at n = 26) when WIDE (B even, 16-B aligned out).
 // (A persistent grid-stride variant was measured slower: the loop made hipcc keep the twiddle
 // words in SGPRs across tiles and spill.)
-template <int L, int N3, bool WIDE, bool CANON, bool LAZY>
+template <int L, int N3, bool WIDE, bool CANON, bool LAZY, bool SIGNBIT = false>
 __global__ __launch_bounds__(gen_block<L>())
 __attribute__((amdgpu_waves_per_eu(gen_waves<L, CANON, LAZY>(), gen_waves<L, CANON, LAZY>())))
 void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const int64_t* __restrict__ draws,
@@ -254,12 +290,57 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         }
 
         Trunc<LAZY> tr;
+        [[maybe_unused]] RangeTrap rt, rt3;      // SIGNBIT: radix-2 half, first radix-3 level
         int32_t ys[N3];                  // shares (tss' signed values, or canonical residues)
         if constexpr (CANON) {
             transform_canon<L, N3>(raw, T, M, ys);
         } else {
         // ---- fft2_inverse: radix-2 DIT over omega_secrets^-1 on bit-reversed registers ----
         FE x[L];
+        if constexpr (SIGNBIT) {
+            uint32_t xc[L], xn[L];               // residue, sign word (bit 31)
+            static_for<0, L>([&](auto i) {
+                const int32_t s = (int32_t)raw[i];
+                xc[rev_digits(i, 2, LB)] = canon32(s, p);
+                xn[rev_digits(i, 2, LB)] = (uint32_t)s;
+            });
+            static_for<1, LB + 1>([&](auto s) {
+                constexpr int H = 1 << (s - 1), LEN = 2 * H;
+                static_for<0, L, LEN>([&](auto g) {
+                    static_for<0, H>([&](auto i) {
+                        constexpr int a = g + i, b = g + i + H;
+                        const uint32_t cu = xc[a], nu = xn[a], cc = xc[b], nc = xn[b];
+                        if constexpr (i == 0) {
+                            const uint32_t t = cu + cc, d1 = t - p;           // bit 31: cu + cc < p
+                            const uint32_t d2 = cu - cc;                      // bit 31: cu < cc
+                            xc[a] = min(t, d1);
+                            xn[a] = maj3(nu, nc, d1);
+                            xc[b] = min(d2, d2 + p);
+                            xn[b] = maj3_nb(nu, nc, d2);
+                        } else {
+                            rt.mul1(cc, T.big2);
+                            const uint32_t tc = montu<true>(T.tw2_m[H - 1 + i], cc, M);
+                            xc[a] = addm(cu, tc, p);
+                            xc[b] = subm(cu, tc, p);
+                            xn[a] = nc;
+                            xn[b] = ~nc;
+                        }
+                        // a zero residue is wrong only as 0 with the sign set (a nonzero multiple of p);
+                        // the first butterfly's u is the structural value 0 (values[0]): (0 +- c) % p is
+                        // exact for c = 0 too, so sparse secrets do not trip the trap there
+                        if constexpr (!(s == 1 && g == 0)) {
+                            rt.out1(xc[a]);
+                            rt.out1(xc[b]);
+                        }
+                    });
+                });
+            });
+            // x * len_inv % p keeps x's sign; the radix-3 half takes tss' signed values again
+            static_for<0, L>([&](auto i) {
+                const uint32_t c = montu<true>(T.linv_m, xc[i], M);      // 0 only for x = 0: exact
+                x[i] = FE{(int32_t)(c - (p & (uint32_t)((int32_t)xn[i] >> 31))), c};
+            });
+        } else {
         static_for<0, L>([&](auto i) {
             const int32_t s = (int32_t)raw[i];
             x[rev_digits(i, 2, LB)] = FE{s, canon32(s, p)};
@@ -282,6 +363,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
             const uint32_t c = montu<LAZY>(T.linv_m, x[i].c, M);
             x[i] = FE{tr(c, (uint32_t)x[i].s, p), c};
         });
+        }
 
         // ---- fft3: radix-3 DIT over omega_shares on digit-reversed, zero-extended registers ----
         FE y[N3];
@@ -302,6 +384,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                         y[g + i + 2 * th] = y[g + i];
                     } else {
                         const FE bb = y[g + i], cc = y[g + i + th], dd = y[g + i + 2 * th];
+                        if constexpr (zd && SIGNBIT && s == 1) rt3.mul1(cc.c, T.big3);
                         FE r[3];
                         static_for<0, 3>([&](auto q) {
                             constexpr int j = i + q * th;
@@ -317,6 +400,11 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                                     const uint32_t c = addm(addm(bb.c, cc.c, p), dd.c, p);
                                     r[q] = FE{tr(c, hi32(v), p), c};
                                 }
+                            } else if constexpr (zd && SIGNBIT && s == 1) {
+                                // first level, b + x c: the sign of c when |c| >= big3 (RangeTrap: c is
+                                // checked against big3 below, the residue for 0)
+                                const uint32_t c = addm(bb.c, montu<LAZY>(T.tw3_m[OB + j], cc.c, M), p);
+                                r[q] = FE{tr(c, (uint32_t)cc.s, p), c};
                             } else if constexpr (zd) {
                                 const int32_t xw = (int32_t)T.tw3[OB + j];
                                 const int64_t v = (int64_t)bb.s + (int64_t)xw * cc.s;
@@ -346,7 +434,9 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         }
 
         if constexpr (LAZY) {                    // a -p under lazy truncation (see Trunc): same rule
-            const uint32_t z = tr.bad(p) ? 1u : 0u;
+            bool trapped = tr.bad(p);
+            if constexpr (SIGNBIT) trapped = trapped || rt.bad(T.big2, p) || rt3.bad(T.big3, p);
+            const uint32_t z = trapped ? 1u : 0u;
             const auto zx = __builtin_amdgcn_permlane32_swap(z, z, false, false);
             const bool pair_zero = z || (half ? zx[0] : zx[1]);
             if (pair_ok && pair_zero) {
@@ -391,7 +481,10 @@ static void gen_launch_mode(const PackedGenArgs& a, uint32_t k, uint32_t t, uint
     constexpr int BS = gen_block<L>();
     const dim3 grid((unsigned)((B + BS - 1) / BS), (unsigned)a.n_vectors);
     const bool wide = B % 2 == 0 && ((uintptr_t)a.out % 16) == 0;
-    if (wide && !CANON && p >= kLazyTruncMinP)          // exact shares, lazy zero handling
+    if (wide && !CANON && p >= kLazyTruncMinP && a.signbit)   // exact shares, sign-bit radix-2 half
+        hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, false, true, true>), grid, dim3(BS), 0, s, a.secrets,
+                           a.dimension, a.draws, a.out, k, t, B, T, log.count);
+    else if (wide && !CANON && p >= kLazyTruncMinP)          // exact shares, lazy zero handling
         hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, false, true>), grid, dim3(BS), 0, s, a.secrets,
                            a.dimension, a.draws, a.out, k, t, B, T, log.count);
     else if (wide)
@@ -527,7 +620,12 @@ hipError_t launch_packed_generate(const PackedGenArgs& args, uint32_t k, uint32_
         const GenTables T = make_gen_tables(L, N3, p, omega_secrets, omega_shares);
         hipError_t e = ensure_table(tab, key, &T, sizeof(T));
         if (e != hipSuccess) return e;
+        // the sign-bit kernel when its range traps stay rare (every multiplied operand must reach
+        // ceil(p / w); bounds above 2^12 would send a measurable share of batches to the fix-up)
+        tab.flags = (T.big2 <= 4096 && T.big3 <= 4096) ? 1u : 0u;
     }
+    const char* sb = getenv("SDA_GEN_SIGNBIT");                 // A/B knob: 0 = the mad_i64 sign kernel
+    a.signbit = (tab.flags & 1u) && !(sb && sb[0] == '0');
     const GenTables* T = static_cast<const GenTables*>(tab.dev);
     GenFixupLog log{static_cast<unsigned int*>(log_buf),
                     reinterpret_cast<uint64_t*>(static_cast<unsigned int*>(log_buf) + 16), kGenLogCap};

@@ -212,8 +212,10 @@ hipError_t launch_packed_reveal_wide(const PackedRevealArgs& a, const uint64_t* 
     if (B == 0 || a.n_vectors == 0) return hipSuccess;
     const uint32_t m = n_idx + 1;
     const int64_t P = p;
-    std::vector<uint8_t> key(sizeof(uint32_t) * 6 + sizeof(uint64_t) * n_idx);
-    const uint32_t kv[6] = {0x57494445u /* wide */, n_idx, k, p, omega_secrets, omega_shares};
+    // mode is part of the key: a CANONICAL call must see the duplicate-point refusal below even when an
+    // EXACT call already built the table for the same clerk set
+    std::vector<uint8_t> key(sizeof(uint32_t) * 7 + sizeof(uint64_t) * n_idx);
+    const uint32_t kv[7] = {0x57494445u /* wide */, n_idx, k, p, omega_secrets, omega_shares, (uint32_t)mode};
     memcpy(key.data(), kv, sizeof(kv));
     memcpy(key.data() + sizeof(kv), indices, sizeof(uint64_t) * n_idx);
     if (tab.key != key) {

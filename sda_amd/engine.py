@@ -79,6 +79,12 @@ SIGNATURES = [
     ("sda_combine_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp, _vp]),
     ("sda_combine_finalize_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, _vp, _vp]),
     ("sda_combine_accumulate_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp, _vp]),
+    ("sda_combine_split_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp, _vp, _vp]),
+    ("sda_combine_split_prefix_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp, _vp, _vp,
+                                           _vp]),
+    ("sda_combine_split_replay_dev", _st, [_vp, C.c_int64, _vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                           _vp, _vp, _vp]),
+    ("sda_combine_split_resolve_dev", _st, [_vp, C.c_int64, _vp, _vp, C.c_uint64, _vp, _vp]),
     ("sda_packed_generate_dev", _st, [_vp, C.POINTER(S.SharingSchemeC), _vp, C.c_uint64, C.c_uint64, _vp, _vp,
                                       _vp]),
     ("sda_packed_generate_mode_dev", _st, [_vp, C.POINTER(S.SharingSchemeC), _vp, C.c_uint64, C.c_uint64, _vp,
@@ -311,6 +317,24 @@ class Engine:
 
     def combine_finalize_dev(self, modulus, sums_ptr, dim, out_ptr, stream=None):
         _check(self.lib.sda_combine_finalize_dev(self.h, modulus, sums_ptr, dim, out_ptr, stream))
+
+    # participation split of the combine (sda_amd.distributed; include/sda_engine.h "participation split")
+    def combine_split_dev(self, modulus, shares_ptr, n, dim, row_stride, inout_ptr, flags_ptr, stream=None):
+        _check(self.lib.sda_combine_split_dev(self.h, modulus, shares_ptr, n, dim, row_stride, inout_ptr, flags_ptr,
+                                              stream))
+
+    def combine_split_prefix_dev(self, modulus, gathered_ptr, world, rank, dim, c_in_ptr, total_ptr, code_ptr,
+                                 stream=None):
+        _check(self.lib.sda_combine_split_prefix_dev(self.h, modulus, gathered_ptr, world, rank, dim, c_in_ptr,
+                                                     total_ptr, code_ptr, stream))
+
+    def combine_split_replay_dev(self, modulus, shares_ptr, n, dim, row_stride, rank, state_ptr, code_ptr,
+                                 stream=None):
+        _check(self.lib.sda_combine_split_replay_dev(self.h, modulus, shares_ptr, n, dim, row_stride, rank,
+                                                     state_ptr, code_ptr, stream))
+
+    def combine_split_resolve_dev(self, modulus, total_ptr, code_ptr, dim, out_ptr, stream=None):
+        _check(self.lib.sda_combine_split_resolve_dev(self.h, modulus, total_ptr, code_ptr, dim, out_ptr, stream))
 
     def packed_generate_dev(self, scheme, secrets_ptr, dimension, n_vectors, draws_ptr, out_ptr, stream=None):
         s = scheme.c()

@@ -14,12 +14,17 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-# (rows, dim) of the participation-split cases: a ragged small one and a 1000 x 100k block
-CASES = [(37, 129), (1000, 100_003)]
-TILE = 128
 MOD = 2147482801
+# participation-split cases (name, rows, dim, modulus, lo, hi): non-negative shares (one reduce) and
+# signed shares (real Additive clerk jobs, additive.rs:46: the exact two-pass split), ragged and 1000 x 100k,
+# a tiny modulus (sign events almost every step) and raw i64 values outside (-m, m) (generic kernel path)
+CASES = [("nonneg", 37, 129, MOD, 0, MOD), ("nonneg", 1000, 100_003, MOD, 0, MOD),
+         ("signed", 37, 129, MOD, -(MOD - 1), MOD), ("signed", 1000, 100_003, MOD, -(MOD - 1), MOD),
+         ("small_m", 203, 4_099, 7, -6, 7), ("raw_i64", 64, 20_001, 1000003, -(1 << 61), 1 << 61)]
+TILE = 128
 SEEDS = (np.arange(48 * 4, dtype=np.int64).reshape(48, 4) * 7919 + 11) % (1 << 31)
 SIGNED = (301, 50_001)
+SEEDS10M = (np.arange(8 * 4, dtype=np.int64).reshape(8, 4) * 104729 + 7) % (1 << 31)
 
 
 def main():
@@ -36,18 +41,20 @@ def main():
     eng = Engine(0)
     dev = torch.device("cuda", 0)
     res = {}
-    for N, D in CASES:
+    for name, N, D, m, lo, hi in CASES:
         s0, cnt = Dd.shard_range(N, rank, world)
-        mine = torch.from_numpy(synth.fill(cnt, D, 0x5DA + 21, 0, MOD, row0=s0)).to(dev)
+        mine = torch.from_numpy(synth.fill(cnt, D, 0x5DA + 21, lo, hi, row0=s0)).to(dev)
         part = torch.empty(D, dtype=torch.int64, device=dev)
         out = torch.empty(D, dtype=torch.int64, device=dev)
-        Dd.combine_rows_sharded(eng, MOD, mine.data_ptr(), cnt, D, D, part, out)
-        res[f"rows_{N}x{D}"] = out.cpu().numpy()
+        st = Dd.SplitStats()
+        Dd.combine_rows_sharded(eng, m, mine.data_ptr(), cnt, D, D, part, out, stats=st)
+        res[f"rows_{name}_{N}x{D}"] = out.cpu().numpy()
+        res[f"signed_{name}_{N}x{D}"] = np.array(st.signed)
         # the same participations streamed as row tiles (configs[3]'s accumulate on every rank)
         tiles = [(mine[t0].data_ptr(), min(TILE, cnt - t0)) for t0 in range(0, cnt, TILE)]
         out2 = torch.empty(D, dtype=torch.int64, device=dev)
-        Dd.combine_tiles_sharded(eng, MOD, tiles, D, D, part, out2)
-        res[f"tiles_{N}x{D}"] = out2.cpu().numpy()
+        Dd.combine_tiles_sharded(eng, m, tiles, D, D, part, out2)
+        res[f"tiles_{name}_{N}x{D}"] = out2.cpu().numpy()
         del mine
 
     # recipient's ChaCha mask combine, seeds split over the ranks + one reduce
@@ -58,6 +65,15 @@ def main():
     out = torch.empty(D, dtype=torch.int64, device=dev)
     Dd.mask_combine_sharded(eng, MOD, D, seeds, part, out)
     res["mask"] = out.cpu().numpy()
+    # configs[4]'s dimension: 8 seeds x 10M-dim, split over the ranks
+    D = 10_000_000
+    s0, cnt = Dd.shard_range(SEEDS10M.shape[0], rank, world)
+    seeds = torch.from_numpy(SEEDS10M[s0:s0 + cnt].astype(np.int32)).to(dev)
+    part = torch.empty(D, dtype=torch.int64, device=dev)
+    out = torch.empty(D, dtype=torch.int64, device=dev)
+    Dd.mask_combine_sharded(eng, MOD, D, seeds, part, out)
+    res["mask10M"] = out.cpu().numpy()
+    del part, out
 
     # signed (order-dependent) combine: column split + all-gather
     N, D = SIGNED

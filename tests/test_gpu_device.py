@@ -198,3 +198,103 @@ def test_packed_reveal_fixup_overflow(engine, oracle):
     assert rc == 0
     for j, b in enumerate(sample):
         assert_same(got[b * k:(b + 1) * k], exp[j * k:(j + 1) * k])
+
+
+def _split_on_one_gpu(engine, m, x, G, tile=None):
+    """The participation split of sda_amd.distributed run for G simulated ranks on one GPU, every step
+    through the C ABI: pass 1 + flags per rank, the all-gather / SUM / MAX exchanges done with torch
+    on the device, prefix + replay + resolve per rank.  Returns (flags, result seen by every rank)."""
+    from sda_amd import distributed as Dd
+    N, D = x.shape
+    spans = [Dd.shard_range(N, g, G) for g in range(G)]
+    tile = tile or N
+
+    def tiles(g):
+        s0, cnt = spans[g]
+        return [(x[s0 + t0].data_ptr(), min(tile, cnt - t0)) for t0 in range(0, cnt, tile)]
+
+    parts = torch.zeros((G, D), dtype=torch.int64, device="cuda")
+    flags = torch.zeros((G, 2), dtype=torch.int64, device="cuda")
+    for g in range(G):
+        for ptr, n in tiles(g):
+            engine.combine_split_dev(m, ptr, n, D, x.stride(0), parts[g].data_ptr(), flags[g].data_ptr(), _stream())
+    fl = flags.sum(dim=0).tolist()
+    states = torch.empty((G, D), dtype=torch.int64, device="cuda")
+    totals = torch.empty((G, D), dtype=torch.int64, device="cuda")
+    codes = torch.empty((G, D), dtype=torch.int32, device="cuda")
+    for g in range(G):
+        engine.combine_split_prefix_dev(m, parts.data_ptr(), G, g, D, states[g].data_ptr(), totals[g].data_ptr(),
+                                        codes[g].data_ptr(), _stream())
+        if g:
+            for ptr, n in tiles(g):
+                engine.combine_split_replay_dev(m, ptr, n, D, x.stride(0), g, states[g].data_ptr(),
+                                                codes[g].data_ptr(), _stream())
+    code = codes.max(dim=0).values.contiguous()
+    outs = torch.empty((G, D), dtype=torch.int64, device="cuda")
+    for g in range(G):
+        engine.combine_split_resolve_dev(m, totals[g].data_ptr(), code.data_ptr(), D, outs[g].data_ptr(), _stream())
+    torch.cuda.synchronize()
+    assert (outs == outs[0]).all()            # every rank resolves the same result
+    return fl, outs[0].cpu().numpy()
+
+
+@pytest.mark.parametrize("m,N,D,lo,hi,G,tile", [
+    (2147482801, 2000, 100_003, -(2147482801 - 1), 2147482801, 8, None),   # signed field shares, 8 ranks
+    (2147482801, 999, 50_000, -(2147482801 - 1), 2147482801, 3, 100),      # row tiles, ragged ranks
+    (7, 1200, 20_002, -6, 7, 8, None),                                     # sign events almost every step
+    ((1 << 62) - 57, 400, 10_001, -((1 << 62) - 58), (1 << 62) - 57, 2, 64),  # largest fast-path moduli
+    (1000003, 300, 9_999, -(1 << 61), 1 << 61, 5, None),                   # raw i64: the generic path
+    (433, 1, 1_001, -432, 433, 1, None),                                   # one rank, one row
+    (433, 3, 4_096, -432, 433, 8, None),                                   # ranks with no rows
+])
+def test_participation_split_signed_exact(engine, oracle, m, N, D, lo, hi, G, tile):
+    """The exact signed participation split (SURVEY §7 hard part 1 (b)): pass-1 flags,
+    prefix, replay of the sign events and their MAX resolution give the reference's single sequential
+    pass (combiner.rs:16-28) bit for bit on signed inputs, whose result depends on the order."""
+    x = torch.empty((N, D), dtype=torch.int64, device="cuda")
+    engine.synth_fill_dev(x.data_ptr(), N, D, 0x5DA + 31, lo, hi, _stream())
+    fl, got = _split_on_one_gpu(engine, m, x, G, tile)
+    xh = x.cpu().numpy()
+    exp = oracle.combine(m, xh)
+    assert fl[0] > 0 and fl[1] == 0
+    assert (exp < 0).any() and (exp > 0).any()
+    assert_same(got, exp)
+
+
+def test_participation_split_flags(engine):
+    """Pass-1 flags: none for non-negative inputs (the one-reduce path), [neg] for a single negative
+    value, [wrap] for a value past 2^63 - m (the split refuses it), in any column and row."""
+    m, N, D = 2147482801, 70, 3_001
+    x = torch.empty((N, D), dtype=torch.int64, device="cuda")
+    engine.synth_fill_dev(x.data_ptr(), N, D, 0x5DA + 32, 0, m, _stream())
+
+    def flags():
+        f = torch.zeros(2, dtype=torch.int64, device="cuda")
+        acc = torch.zeros(D, dtype=torch.int64, device="cuda")
+        engine.combine_split_dev(m, x.data_ptr(), N, D, D, acc.data_ptr(), f.data_ptr(), _stream())
+        torch.cuda.synchronize()
+        return f.tolist(), acc
+    f, acc = flags()
+    assert f == [0, 0]
+    assert torch.equal(acc, torch.remainder(x.sum(dim=0), m))
+    x[69, 3000] = -1
+    assert flags()[0] == [1, 0]
+    x[69, 3000] = 5
+    x[13, 1] = (1 << 63) - m + 1            # just past the no-wrap range
+    assert flags()[0] == [0, 1]
+    x[13, 1] = (1 << 63) - m                # the range's edge: fine
+    assert flags()[0] == [0, 0]
+    x[0, 0] = -(1 << 63)
+    assert flags()[0] == [1, 1]
+
+
+def test_finalize_signed_sums(engine):
+    """sda_combine_finalize_dev takes signed int64 sums (the all-reduced per-rank results) to their
+    canonical residue -- negative sums included (it once read them as u64)."""
+    m = 2147482801
+    s = torch.tensor([-1, -m, -(m + 1), -(8 * (m - 1)), 8 * (m - 1), 0, m - 1, -(1 << 62)], dtype=torch.int64,
+                     device="cuda")
+    out = torch.empty_like(s)
+    engine.combine_finalize_dev(m, s.data_ptr(), s.numel(), out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    assert out.tolist() == [int(v) % m for v in s.tolist()]

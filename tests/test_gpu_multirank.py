@@ -56,20 +56,30 @@ def results(request, tmp_path_factory):
         return {k: z[k] for k in z.files}
 
 
-@pytest.mark.parametrize("N,D", W.CASES)
-def test_sharded_rows_and_tiles_equal_single_pass(results, oracle, N, D):
-    """combine_rows_sharded / combine_tiles_sharded: participation split, one int64 all-reduce,
-    device `% m` == the single sequential pass over all N rows."""
-    full = synth.fill(N, D, 0x5DA + 21, 0, W.MOD)
-    exp = oracle.combine(W.MOD, full)
-    assert np.array_equal(results[f"rows_{N}x{D}"], exp)
-    assert np.array_equal(results[f"tiles_{N}x{D}"], exp)
+@pytest.mark.parametrize("name,N,D,m,lo,hi", W.CASES)
+def test_sharded_rows_and_tiles_equal_single_pass(results, oracle, name, N, D, m, lo, hi):
+    """combine_rows_sharded / combine_tiles_sharded: participation split == the single sequential pass
+    over all N rows -- non-negative shares through one int64 all-reduce + device `% m`, signed shares
+    through the exact two-pass split (replay + MAX-resolved sign events)."""
+    full = synth.fill(N, D, 0x5DA + 21, lo, hi)
+    exp = oracle.combine(m, full)
+    assert bool(results[f"signed_{name}_{N}x{D}"]) == (lo < 0)
+    if lo < 0:
+        assert (exp < 0).any()
+    assert np.array_equal(results[f"rows_{name}_{N}x{D}"], exp)
+    assert np.array_equal(results[f"tiles_{name}_{N}x{D}"], exp)
 
 
 def test_sharded_mask_combine_seed_split(results, oracle):
     """mask_combine_sharded: the recipient's ChaCha mask combine over seeds split across ranks."""
     exp = oracle.chacha_mask_combine(W.MOD, 70_001, W.SEEDS)
     assert np.array_equal(results["mask"], exp)
+
+
+def test_sharded_mask_combine_10M(results, oracle):
+    """mask_combine_sharded at configs[4]'s dimension (8 seeds x 10M-dim split over the ranks)."""
+    exp = oracle.chacha_mask_combine(W.MOD, 10_000_000, W.SEEDS10M)
+    assert np.array_equal(results["mask10M"], exp)
 
 
 def test_sharded_signed_column_split(results, oracle):
@@ -80,3 +90,25 @@ def test_sharded_signed_column_split(results, oracle):
     exp = oracle.combine(W.MOD, x)
     assert (exp < 0).any()
     assert np.array_equal(results["columns"], exp)
+
+
+def test_bench_spawns_its_own_ranks(tmp_path):
+    """`bench.py --gpus 2` with no launcher starts its two ranks itself (gloo rehearsal: both share
+    cuda:0) and rank 0 prints the JSON line with n_gpus = 2; the signed participation-split leg runs
+    and checks itself.  A mismatched WORLD_SIZE exits non-zero instead of benchmarking one GPU."""
+    import json
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, SDA_DIST_BACKEND="gloo", PYTHONUNBUFFERED="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--no-side", "--no-cpu", "--steps", "2",
+           "--warmup", "1", "--rows", "64", "--dim", "200000"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=170)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["value"] > 0
+    assert rec["combine_signed_split"]["passes"] == 2
+    bad = subprocess.run(cmd, env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), capture_output=True,
+                         text=True, timeout=120)
+    assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr

@@ -390,6 +390,39 @@ def test_packed_generate_negative_multiple_of_p(engine, oracle, sch):
     assert_same(got, oracle.packed_generate(_pp(oracle, sch), secrets, draws))
 
 
+@pytest.mark.parametrize("sch", [s for s in packed_schemes() if s.prime_modulus >= 2**24],
+                         ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")
+def test_packed_generate_structured_values(engine, oracle, sch):
+    """Exact share-gen on structured batches that stress the sign-bit radix-2 half (packed_gen.hip,
+    SIGNBIT) and its traps: sparse vectors (zero secrets; all-zero batches), tiny values (+-1, +-2, where
+    the twiddle products no longer dominate), values a and p - a of either sign (butterfly sums that are
+    exact multiples of p, where tss truncates to 0), and p - 1 -- mixed with random batches.  Every batch
+    must equal the oracle (tss' operation order) whatever path -- fast or fix-up -- it took."""
+    p, k, t = sch.prime_modulus, sch.secret_count, sch.privacy_threshold()
+    L = k + t + 1
+    rng = np.random.default_rng(p % 7919 + 3 * L)
+    B = 4096
+    raw = rng.integers(-(p - 1), p, size=(B, L), dtype=np.int64)
+    a = int(rng.integers(3, p - 3))
+    pool = np.array([0, 1, -1, 2, -2, a, -a, p - a, -(p - a), p - 1, -(p - 1)], dtype=np.int64)
+    for b in range(B):
+        kind = b % 4
+        if kind == 0:                        # sparse: a few pool values, the rest zero
+            raw[b] = 0
+            pos = rng.choice(np.arange(1, L), size=int(rng.integers(1, min(4, L - 1) + 1)), replace=False)
+            raw[b, pos] = rng.choice(pool, size=pos.size)
+        elif kind == 1:                      # every value from the pool
+            raw[b] = rng.choice(pool, size=L)
+        elif kind == 2:                      # zero secrets, random draws
+            raw[b, 1:k + 1] = 0
+        raw[b, 0] = 0                        # values[0] = 0 (the inserted point)
+    raw[-1] = 0                              # an all-zero batch
+    secrets = raw[:, 1:k + 1].reshape(-1).copy()
+    draws = raw[:, k + 1:].reshape(-1).copy()
+    got = engine.share_generate(sch, secrets, draws)
+    assert_same(got, oracle.packed_generate(_pp(oracle, sch), secrets, draws))
+
+
 @pytest.mark.parametrize("sch", [s for s in packed_schemes() if s.prime_modulus >= 2**24 and
                                  s.secret_count <= 8 and s.reconstruction_threshold() <= 15],
                          ids=lambda s: f"k{s.secret_count}t{s.privacy_threshold()}n{s.share_count}")

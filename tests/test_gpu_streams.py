@@ -43,6 +43,37 @@ def test_calls_on_two_streams_share_scratch_safely(engine, oracle):
         assert_same(gb[:, b], oracle.packed_share(pp, sec_b[b * k:(b + 1) * k], dr[b]))
 
 
+def test_stream_destroyed_between_calls(engine, oracle):
+    """A caller that creates and destroys a HIP stream per call (a C consumer, a torch ExternalStream):
+    the next call on another stream orders itself after the previous call through an event recorded
+    when that call returned, so it never touches the destroyed stream."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")          # the runtime torch already loaded (one soname)
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    m, N, D = 2147482801, 33, 10_001
+    x = np.random.default_rng(5).integers(-(m - 1), m, size=(N, D), dtype=np.int64)
+    xd = torch.from_numpy(x).cuda()
+    exp = oracle.combine(m, x)
+    outs = []
+    torch.cuda.synchronize()
+    for i in range(4):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        o = torch.empty(D, dtype=torch.int64, device="cuda")
+        engine.combine_dev(m, xd.data_ptr(), N, D, D, o.data_ptr(), s.value)
+        if i % 2:
+            assert hip.hipStreamSynchronize(s) == 0
+        assert hip.hipStreamDestroy(s) == 0      # destroyed with (i even) or without its work drained
+        outs.append(o)
+    o = torch.empty(D, dtype=torch.int64, device="cuda")
+    engine.combine_dev(m, xd.data_ptr(), N, D, D, o.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for r in outs + [o]:
+        assert_same(r.cpu().numpy(), exp)
+
+
 @pytest.mark.parametrize("m", [2147482801, (1 << 40) + 7])
 def test_chacha_stream_path_equals_fast_path(engine, m, monkeypatch):
     """Both exact ChaCha implementations (counter mode + rejection fix-up, and per-stream expansion +

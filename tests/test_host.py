@@ -60,39 +60,77 @@ def _run_world2(target, world=2):
     return res
 
 
+def _split_cases():
+    """(name, modulus, N, D, lo, hi): non-negative (configs[3]), signed field shares (real Additive
+    clerk jobs, additive.rs:46), a tiny modulus (sign events in almost every step), a 2^40-class
+    modulus, and raw i64 values far outside (-m, m) (the generic path; within the no-wrap range)."""
+    return [("nonneg", 2147482801, 37, 129, 0, 2147482801),
+            ("signed", 2147482801, 37, 129, -(2147482801 - 1), 2147482801),
+            ("small_m", 7, 41, 66, -6, 7),
+            ("m2_40", (1 << 40) + 15, 29, 50, -(1 << 40), (1 << 40) + 15),
+            ("raw_i64", 1000003, 23, 31, -(1 << 61), 1 << 61)]
+
+
 def _worker_rows(rank, world, port, q):
     """sda_amd.distributed.combine_rows_sharded / combine_tiles_sharded themselves (participation
-    split, int64 all-reduce, finalize) with the oracle as the per-rank compute (tests/cpu_engine)."""
+    split: pass 1 + flags, one int64 all-reduce, finalize -- or, for signed inputs, the two-pass
+    replay + MAX-resolved sign events) with the oracle as the per-rank compute (tests/cpu_engine)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle as O
     from tests.cpu_engine import CpuEngine
-    eng = CpuEngine()
-    m, N, D = 2147482801, 37, 129
-    full = torch.from_numpy(synth.fill(N, D, 0x5DA + 4, 0, m))      # non-negative inputs (configs[3])
-    start, count = Dd.shard_range(N, rank, world)
-    mine = full[start:start + count].contiguous()
-    part, out = torch.empty(D, dtype=torch.int64), torch.empty(D, dtype=torch.int64)
-    Dd.combine_rows_sharded(eng, m, mine.data_ptr(), count, D, D, part, out)
-    res = {"rows": (out.tolist(), O.combine(m, full.numpy()).tolist())}
-    # the same rows streamed as 5-row tiles (configs[3]'s tiled accumulate on each rank)
-    tiles = [(mine[t0].data_ptr(), min(5, count - t0)) for t0 in range(0, count, 5)]
-    Dd.combine_tiles_sharded(eng, m, tiles, D, D, part, out)
-    res["tiles"] = (out.tolist(), res["rows"][1])
-    res["calls"] = sorted(set(eng.calls))
+    res = {}
+    for name, m, N, D, lo, hi in _split_cases():
+        eng = CpuEngine()
+        full = torch.from_numpy(synth.fill(N, D, 0x5DA + 4, lo, hi))
+        start, count = Dd.shard_range(N, rank, world)
+        mine = full[start:start + count].contiguous()
+        part, out = torch.empty(D, dtype=torch.int64), torch.empty(D, dtype=torch.int64)
+        exp = O.combine(m, full.numpy()).tolist()
+        st = Dd.SplitStats()
+        Dd.combine_rows_sharded(eng, m, mine.data_ptr(), count, D, D, part, out, stats=st)
+        res[name + "/rows"] = (out.tolist(), exp, st.signed)
+        # the same rows streamed as 5-row tiles (configs[3]'s tiled accumulate on each rank)
+        tiles = [(mine[t0].data_ptr(), min(5, count - t0)) for t0 in range(0, count, 5)]
+        Dd.combine_tiles_sharded(eng, m, tiles, D, D, part, out, stats=st)
+        res[name + "/tiles"] = (out.tolist(), exp, st.signed)
+        calls = [None] * world
+        dist.all_gather_object(calls, sorted(set(eng.calls)))
+        res[name + "/calls"] = sorted(set(c for cs in calls for c in cs))
+    # an input the reference's running sum could wrap on: the split refuses it (never a wrong value)
+    m = 1000003
+    x = torch.from_numpy(synth.fill(4, 8, 1, 0, 100))
+    if rank == 1:
+        x[2, 3] = (1 << 63) - 5
+    part, out = torch.empty(8, dtype=torch.int64), torch.empty(8, dtype=torch.int64)
+    try:
+        Dd.combine_rows_sharded(CpuEngine(), m, x.data_ptr(), 4, 8, 8, part, out)
+        res["wrap_refused"] = False
+    except ValueError:
+        res["wrap_refused"] = True
     if rank == 0:
         q.put(res)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_sharded_combine_matches_single_pass(world):
-    """combine_rows_sharded and combine_tiles_sharded at world size 2 and 8 (gloo; 8 = the driver's
-    node) equal the reference's single sequential pass (combiner.rs:16-28) for non-negative inputs."""
+    """combine_rows_sharded and combine_tiles_sharded at world sizes 2, 3 and 8 (gloo; 8 = the
+    driver's node) equal the reference's single sequential pass (combiner.rs:16-28) bit for bit --
+    non-negative AND signed inputs (the two-pass split), raw i64 inputs, tiny moduli -- and refuse
+    inputs where the reference's own sum may wrap."""
     res = _run_world2(_worker_rows, world)
-    assert res["rows"][0] == res["rows"][1]
-    assert res["tiles"][0] == res["tiles"][1]
-    assert res["calls"] == ["combine_accumulate_dev", "combine_dev", "combine_finalize_dev"]
+    assert res.pop("wrap_refused") is True
+    split = ["combine_finalize_dev", "combine_split_dev"]
+    two_pass = ["combine_split_dev", "combine_split_prefix_dev", "combine_split_replay_dev",
+                "combine_split_resolve_dev"]
+    for name, *_ in _split_cases():
+        for kind in ("rows", "tiles"):
+            got, exp, signed = res[name + "/" + kind]
+            assert got == exp, (name, kind)
+            assert signed == (name != "nonneg"), (name, kind)
+        calls = res[name + "/calls"]
+        assert calls == (split if name == "nonneg" else two_pass), (name, calls)
 
 
 def _worker_mask_columns(rank, world, port, q):
