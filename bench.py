@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--seeds", type=int, default=100_000, help="configs[4]: participant seeds in total")
     ap.add_argument("--rows", type=int, default=10_000, help="participations per GPU (configs[1]: 10k)")
     ap.add_argument("--dim", type=int, default=1_000_000, help="vector dimension (configs[1]: 1M)")
-    ap.add_argument("--shamir-vectors", type=int, default=64, help="participant vectors per share-gen launch")
+    ap.add_argument("--shamir-vectors", type=int, default=1000,
+                    help="participant vectors per share-gen / reveal launch (BASELINE.md C3: P = 1,000)")
     ap.add_argument("--chacha-seeds", type=int, default=256)
     ap.add_argument("--no-side", action="store_true", help="skip packed-Shamir / ChaCha legs")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")

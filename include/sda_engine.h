@@ -24,8 +24,10 @@
  *     are not Sync either); distinct handles are independent.  The handle's
  *     scratch buffers are shared by its calls: a `_dev` call on a different
  *     stream than the handle's previous call first makes its stream wait (an
- *     event, no host sync) for the work queued on the previous one, so calls
- *     on one handle never race however the caller mixes streams.
+ *     event recorded when the previous call returned, no host sync) for the
+ *     work queued by the previous one, so calls on one handle never race
+ *     however the caller mixes streams.  The previous call's stream is not
+ *     touched again: it may be destroyed once that call has returned.
  */
 #ifndef SDA_ENGINE_H
 #define SDA_ENGINE_H
