@@ -584,17 +584,26 @@ def main():
         for i in range(4):
             f = lambda: eng.clerk_decode_combine_dev(m, buf.data_ptr(), off, cout.data_ptr(), Dc, stream())  # noqa
             ct.record(f) if i else f()
-        # the fused column-tile decode+combine (payload read once; measured slower, so opt-in: the
-        # SDA_CODEC_PATH knob), timed beside the default decode-to-int32-matrix + combine
-        mt = Timer(torch)
+        # the other two exact paths, timed beside the default (SDA_CODEC_PATH knob): the count pass + dense
+        # int32 matrix + combine (round 2's default), and the fused column-tile decode+combine (opt-in)
+        alt = {}
         cout_m = torch.empty(Dc, dtype=torch.int64, device=dev)
-        os.environ["SDA_CODEC_PATH"] = "fused"
-        try:
-            for i in range(4):
-                f = lambda: eng.clerk_decode_combine_dev(m, buf.data_ptr(), off, cout_m.data_ptr(), Dc, stream())  # noqa
-                mt.record(f) if i else f()
-        finally:
-            del os.environ["SDA_CODEC_PATH"]
+        prev = os.environ.get("SDA_CODEC_PATH")
+        for pname in ("matrix", "fused"):
+            alt[pname] = Timer(torch)
+            os.environ["SDA_CODEC_PATH"] = pname
+            try:
+                for i in range(4):
+                    f = lambda: eng.clerk_decode_combine_dev(m, buf.data_ptr(), off, cout_m.data_ptr(), Dc, stream())  # noqa
+                    alt[pname].record(f) if i else f()
+            finally:
+                if prev is None:
+                    del os.environ["SDA_CODEC_PATH"]
+                else:
+                    os.environ["SDA_CODEC_PATH"] = prev
+            torch.cuda.synchronize()
+            if not args.no_check and not torch.equal(cout, cout_m):
+                raise SystemExit(f"codec {pname} vs default decode+combine FAILED")
         torch.cuda.synchronize()
         if not args.no_check:
             if not torch.equal(mat, x):
@@ -605,9 +614,9 @@ def main():
             if not (torch.equal(torch.remainder(r, m), torch.remainder(x[:, cols].sum(0), m))
                     and bool((r.abs() < m).all())):
                 raise SystemExit("codec decode+combine FAILED")
-            if not torch.equal(cout, cout_m):
-                raise SystemExit("codec fused vs matrix decode+combine FAILED")
-        e_ms, d_ms, c_ms, cm_ms = et.mean_ms(), dt_.mean_ms(), ct.mean_ms(), mt.mean_ms()
+        e_ms, d_ms, c_ms = et.mean_ms(), dt_.mean_ms(), ct.mean_ms()
+        mx_ms, cm_ms = alt["matrix"].mean_ms(), alt["fused"].mean_ms()
+        default_path = os.environ.get("SDA_CODEC_PATH", "slots")
         side["codec"] = {
             "config": f"varint payloads of {Nc} participations x 1M-dim signed field shares "
                       f"({payload / Nc / Dc:.2f} B/share)",
@@ -616,10 +625,16 @@ def main():
             "decode_hbm_GBps": (payload + 8.0 * Nc * Dc) / (d_ms * 1e-3) / 1e9,
             "decode_combine_ms": c_ms, "decode_combine_shares_per_s": Nc * Dc / (c_ms * 1e-3),
             "decode_combine_payload_GBps": payload / (c_ms * 1e-3) / 1e9,
-            # bytes the three passes move: payload read twice (count, decode), the int32 matrix written and
-            # read back, the i64 result written
-            "decode_combine_hbm_GBps": (2 * payload + 8.0 * Nc * Dc + 8.0 * Dc) / (c_ms * 1e-3) / 1e9,
-            "decode_combine_path": "count pass, decode to an int32 matrix, exact combine",
+            "decode_combine_roofline_frac": (payload + 8.0 * Dc) / (c_ms * 1e-3) / 8.0e12,
+            # bytes the default path moves: payload read once, int32 slots written and read back, the i64
+            # result written (the matrix path reads the payload twice: count pass + decode)
+            "decode_combine_hbm_GBps": ((payload if default_path == "slots" else 2 * payload) + 8.0 * Nc * Dc
+                                        + 8.0 * Dc) / (c_ms * 1e-3) / 1e9,
+            "decode_combine_path": {"slots": "decode once into int32 slots per 16 KiB region, exact combine over "
+                                             "the slots", "matrix": "count pass, decode to an int32 matrix, exact "
+                                             "combine", "fused": "count pass, fused column-tile decode+combine"
+                                    }.get(default_path, default_path),
+            "decode_combine_matrix_ms": mx_ms,
             "decode_combine_fused_ms": cm_ms,
             "encode_ms": e_ms, "encode_hbm_GBps": (payload + 8.0 * Nc * Dc) / (e_ms * 1e-3) / 1e9,
         }

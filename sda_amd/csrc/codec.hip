@@ -295,17 +295,24 @@ __device__ __forceinline__ int64_t varint_value_at(const uint32_t* lb, uint32_t 
 //
 // OutT = int32_t (the clerk's decode -> combine of field shares, |v| < 2^31): the values are stored
 // narrowed and any value that does not fit sets *wide (the caller then decodes again as i64).
-template <typename OutT>
+//
+// SPARSE (the clerk's decode -> combine without a count pass): region r's elements go to its own slots
+// out + r * kRegionBytes (a region of kRegionBytes bytes holds at most that many elements), and the
+// region's element count to region_count[r]; region_base and blob_irregular are not read.  A malformed
+// blob (a run of >= 11 continuation bytes) always holds an element longer than 5 bytes, so it sets *wide.
+template <typename OutT, bool SPARSE = false>
 __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* __restrict__ bytes,
                                                                  const uint64_t* __restrict__ blob_region,
                                                                  const uint64_t* __restrict__ blob_off, uint32_t y0,
                                                                  const uint64_t* __restrict__ region_base,
                                                                  const uint32_t* __restrict__ blob_irregular,
                                                                  OutT* __restrict__ out, uint64_t out_stride,
-                                                                 uint32_t* __restrict__ wide) {
+                                                                 uint32_t* __restrict__ wide,
+                                                                 uint32_t* __restrict__ region_count = nullptr) {
     uint32_t b;
     uint64_t r, word;
-    if (!region_of(blob_region, blob_off, y0, &b, &r, &word) || (blob_irregular[b] & 1u)) return;
+    if (!region_of(blob_region, blob_off, y0, &b, &r, &word)) return;
+    if (!SPARSE && (blob_irregular[b] & 1u)) return;
     // LDS holds one sub-region at a time (the region's other words wait in registers): 12.9 KB per
     // workgroup instead of 26.7, so LDS no longer caps the waves per SIMD
     __shared__ uint32_t lb[(kSubBytes + 32) / 4];             // [halo 16 B | sub-region 4 KiB | tail 16 B]
@@ -328,7 +335,7 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
     uint4 h = make_uint4(0, 0, 0, 0);                         // the word before the region (thread 0)
     if (threadIdx.x == 0 && word * 16 > begin) h = p[word - 1];
     if (threadIdx.x == kThreads - 1) lb4[kThreads + 1] = make_uint4(0, 0, 0, 0);
-    OutT* dst = out + (uint64_t)b * out_stride + region_base[r];
+    OutT* dst = SPARSE ? out + r * kRegionBytes : out + (uint64_t)b * out_stride + region_base[r];
     bool narrow_fail = false;
     uint32_t base = 0;                                        // elements in earlier sub-regions
 #pragma unroll
@@ -400,6 +407,84 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
     if constexpr (sizeof(OutT) < 8) {
         if (narrow_fail) atomicOr(wide, 1u);             // rare: one atomic per lane that saw it
     }
+    if constexpr (SPARSE) {
+        if (threadIdx.x == 0) region_count[r] = base;
+    }
+}
+
+// ---------------- the clerk's decode -> combine over region slots ----------------
+// After the SPARSE decode and varint_scan_kernel (region_base = the blob's elements before region r),
+// element j of blob b sits in the region r of b with region_base[r] <= j < region_base[r] + count[r],
+// at slot r * kRegionBytes + (j - region_base[r]).  The combine walks column tiles of kScTile elements:
+// plan[t * n_blobs + b] = r << 32 | (t * kScTile - region_base[r]), the region holding the tile's first
+// element.  One thread per (region, blob) emits the entries of the tiles whose first element it holds.
+constexpr uint32_t kScTile = 2 * kThreads;
+__global__ __launch_bounds__(kThreads) void slot_plan_kernel(const uint64_t* __restrict__ blob_region,
+                                                             const uint64_t* __restrict__ region_base,
+                                                             const uint32_t* __restrict__ region_count, uint32_t y0,
+                                                             uint64_t n_blobs, uint64_t ntiles,
+                                                             uint64_t* __restrict__ plan) {
+    const uint64_t b = y0 + blockIdx.y;
+    const uint64_t r0 = blob_region[b], r1 = blob_region[b + 1];
+    const uint64_t r = r0 + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (r >= r1) return;
+    const uint64_t E0 = region_base[r], E1 = E0 + region_count[r];
+    for (uint64_t t = (E0 + kScTile - 1) / kScTile; t < ntiles && t * kScTile < E1; ++t)
+        plan[t * n_blobs + b] = (r << 32) | (t * kScTile - E0);
+}
+
+// One workgroup per column tile: lane l owns columns e0 + l and e0 + 256 + l (each load instruction of a
+// wave reads 256 contiguous bytes of a region's slots) and walks the blobs in reference order through
+// combiner.rs:16-28's exact recurrence (add_trem).  A tile's elements lie in at most two regions unless a
+// blob's regions are tiny (then the lane walks on region by region).  Blobs go UNROLL at a time: their plan
+// entries and region counts are uniform (scalar loads), then all their slot loads are issued before the
+// dependent chain.  Every blob decoded to `dim` elements (checked on the host before the launch).
+template <int UNROLL>
+__global__ __launch_bounds__(kThreads) void slot_combine_kernel(const int32_t* __restrict__ slots,
+                                                                const uint64_t* __restrict__ plan,
+                                                                const uint32_t* __restrict__ region_count,
+                                                                uint64_t n_blobs, uint64_t dim,
+                                                                int64_t* __restrict__ out, Mod64 M, bool small_m) {
+    const uint64_t t = blockIdx.x;
+    const uint64_t e0 = t * kScTile;
+    const uint32_t o[2] = {threadIdx.x, threadIdx.x + kThreads};
+    const bool live[2] = {e0 + o[0] < dim, e0 + o[1] < dim};
+    const uint64_t* pl = plan + t * n_blobs;
+    auto slot_of = [&](uint64_t pe, uint32_t off) -> uint64_t {
+        uint64_t r = pe >> 32;
+        uint64_t local = (pe & 0xFFFFFFFFu) + off;
+        uint32_t c = region_count[r];
+        while (local >= c) {                     // the tile's tail lies in the blob's next region(s)
+            local -= c;
+            c = region_count[++r];
+        }
+        return r * kRegionBytes + local;
+    };
+    int64_t acc[2] = {0, 0};
+    uint64_t b = 0;
+    for (; b + UNROLL <= n_blobs; b += UNROLL) {
+        int32_t v[UNROLL][2];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t pe = pl[b + u];
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+                v[u][e] = live[e] ? __builtin_nontemporal_load(slots + slot_of(pe, o[e])) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) acc[e] = add_trem(acc[e], v[u][e], M, small_m);
+    }
+    for (; b < n_blobs; ++b) {
+        const uint64_t pe = pl[b];
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            if (live[e]) acc[e] = add_trem(acc[e], __builtin_nontemporal_load(slots + slot_of(pe, o[e])), M, small_m);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+        if (live[e]) out[e0 + o[e]] = acc[e];
 }
 
 // ---------------- the clerk's fused decode -> combine ----------------
@@ -979,6 +1064,64 @@ hipError_t launch_varint_decode_narrow(const uint8_t* bytes, uint64_t n_blobs, c
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     *wide_host = flag != 0;
     return hipSuccess;
+}
+
+size_t varint_slot_bytes(const VarintPlan& plan, uint64_t n_blobs, uint64_t dim) {
+    const uint64_t ntiles = (dim + kScTile - 1) / kScTile;
+    return plan.regions * kRegionBytes * sizeof(int32_t) + ntiles * n_blobs * 8 + 256;
+}
+
+hipError_t launch_varint_decode_slots(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
+                                      const VarintPlan& plan, void* work, void* slot_buf, uint64_t* counts_host,
+                                      bool* wide_host, hipStream_t s) {
+    const size_t R = plan.regions;
+    DecodeWork w = carve(work, R, n_blobs);
+    int32_t* slots = static_cast<int32_t*>(slot_buf);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(w.blob_off, blob_off_host, (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(w.blob_region, plan.blob_region.data(), (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.wide, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+    for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
+        const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
+        hipLaunchKernelGGL((varint_decode_kernel<int32_t, true>), dim3((unsigned)plan.max_regions, ny), dim3(kThreads),
+                           0, s, bytes, w.blob_region, w.blob_off, (uint32_t)y0, (const uint64_t*)nullptr,
+                           (const uint32_t*)nullptr, slots, 0, w.wide, w.region_count);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(varint_scan_kernel, dim3((unsigned)n_blobs), dim3(kThreads), 0, s, w.region_count,
+                       w.blob_region, w.region_base, w.blob_count);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    uint32_t flag = 0;
+    if ((e = hipMemcpyAsync(counts_host, w.blob_count, n_blobs * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(&flag, w.wide, sizeof(flag), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    *wide_host = flag != 0;
+    return hipSuccess;
+}
+
+hipError_t launch_slot_combine(const VarintPlan& plan, void* work, const void* slot_buf, uint64_t n_blobs,
+                               uint64_t dim, int64_t* out, int64_t modulus, hipStream_t s) {
+    if (dim == 0 || n_blobs == 0) return hipSuccess;
+    const size_t R = plan.regions;
+    DecodeWork w = carve(work, R, n_blobs);
+    const int32_t* slots = static_cast<const int32_t*>(slot_buf);
+    uint64_t* tplan = reinterpret_cast<uint64_t*>(const_cast<char*>(static_cast<const char*>(slot_buf)) +
+                                                  R * kRegionBytes * sizeof(int32_t));
+    const uint64_t ntiles = (dim + kScTile - 1) / kScTile;
+    if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipError_t e;
+    for (uint64_t y0 = 0; y0 < n_blobs; y0 += 65535) {
+        const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
+        hipLaunchKernelGGL(slot_plan_kernel, dim3((unsigned)((plan.max_regions + kThreads - 1) / kThreads), ny),
+                           dim3(kThreads), 0, s, w.blob_region, w.region_base, w.region_count, (uint32_t)y0, n_blobs,
+                           ntiles, tplan);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    const Mod64 M = make_mod64(modulus);
+    const bool small_m = modulus <= ((int64_t)1 << 62);
+    hipLaunchKernelGGL(slot_combine_kernel<8>, dim3((unsigned)ntiles), dim3(kThreads), 0, s, slots, tplan,
+                       w.region_count, n_blobs, dim, out, M, small_m);
+    return hipGetLastError();
 }
 
 hipError_t launch_varint_decode_combine(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,

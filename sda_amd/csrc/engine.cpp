@@ -792,8 +792,47 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
     // 1000 x 1M launch vs 2.2 + 0.7 ms, profiles/r02d/ab_codec_fused.txt); the default is the matrix path.
     const char* path = getenv("SDA_CODEC_PATH");
     const bool force_fused = path && strcmp(path, "fused") == 0, force_matrix = !force_fused;
+    const char* env = getenv("SDA_CODEC_NARROW");                    // "0": A/B and test knob
+    const bool narrow_ok = !(env && atoi(env) == 0);
     sda::VarintPlan plan;
     std::vector<uint64_t> counts(n_blobs);
+    // Default: decode once into int32 slots per 16 KiB region (no count pass), then the exact combine
+    // over the slots.  SDA_CODEC_PATH=matrix (A/B and test knob) takes the count pass + dense int32
+    // matrix path; any element longer than 5 bytes or outside int32 (malformed or raw i64 payloads)
+    // falls back to it as well.
+    if (narrow_ok && !force_fused && !(path && strcmp(path, "matrix") == 0)) {
+        if (((uintptr_t)bytes & 15) != 0) return fail(SDA_ERR_INVALID_ARGUMENT, "byte buffer must be 16-byte aligned");
+        for (uint64_t b = 0; b < n_blobs; ++b)
+            if (blob_off[b + 1] < blob_off[b]) return fail(SDA_ERR_INVALID_ARGUMENT, "blob offsets must be non-decreasing");
+        sda::varint_plan(blob_off, n_blobs, &plan);
+        if (sda_status e = ensure(&h->codec_work, &h->codec_work_bytes,
+                                  sda::varint_decode_work_bytes(plan.regions, n_blobs)))
+            return e;
+        // the slots are sized by the bytes, the tile plan by the dimension (<= the bytes of blob 0)
+        const uint64_t dim_max = blob_off[1] - blob_off[0];
+        if (sda_status e = ensure(&h->codec_mat, &h->codec_mat_bytes, sda::varint_slot_bytes(plan, n_blobs, dim_max)))
+            return e;
+        bool wide = false;
+        HIP_TRY(sda::launch_varint_decode_slots(bytes, blob_off, n_blobs, plan, h->codec_work, h->codec_mat,
+                                                counts.data(), &wide, st));
+        if (!wide) {
+            const uint64_t dim = counts[0];
+            for (uint64_t i = 1; i < n_blobs; ++i)
+                if (counts[i] != dim)
+                    return fail(SDA_ERR_WRONG_DIMENSION,
+                                "Wrong dimension (participation %llu decodes to %llu shares, expected %llu)",
+                                (unsigned long long)i, (unsigned long long)counts[i], (unsigned long long)dim);
+            int64_t mm = 1;
+            if (dim) {
+                if (sda_status e = modulus_abs(m, &mm)) return e;
+            }
+            if (out_cap < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
+            *out_len = dim;
+            if (dim == 0) return ok();
+            HIP_TRY(sda::launch_slot_combine(plan, h->codec_work, h->codec_mat, n_blobs, dim, out, mm, st));
+            return SDA_OK;
+        }
+    }
     bool irregular = false, long_elems = false;
     if (sda_status e = codec_count(h, bytes, blob_off, n_blobs, &plan, counts.data(), &irregular, st, !force_matrix,
                                    &long_elems))
@@ -822,8 +861,6 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
     // Decoded field shares fit in int32 (|share| < m <= 2^31 for every field the reference uses): the
     // [N][dim] matrix between the decode and the combine is stored narrowed, which halves its write and
     // its read.  Any value that does not fit (or a malformed blob) takes the int64 matrix instead.
-    const char* env = getenv("SDA_CODEC_NARROW");                    // "0": A/B and test knob
-    const bool narrow_ok = !(env && atoi(env) == 0);
     if (narrow_ok && !irregular) {
         bool wide = false;
         int32_t* mat32 = static_cast<int32_t*>(h->codec_mat);

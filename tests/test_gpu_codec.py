@@ -182,7 +182,7 @@ def test_continuation_runs_at_every_alignment(engine, oracle, monkeypatch, run):
     assert counts.tolist() == [S] * len(blobs)
     assert_same(out.cpu().numpy(), rows, f"decode run={run}")
     exp = oracle.combine(m, rows)
-    for path in ("matrix", "fused"):
+    for path in ("matrix", "fused", "slots"):
         monkeypatch.setenv("SDA_CODEC_PATH", path)
         res = torch.full((S,), 7, dtype=torch.int64, device="cuda")
         assert engine.clerk_decode_combine_dev(m, t.data_ptr(), off, res.data_ptr(), S) == S

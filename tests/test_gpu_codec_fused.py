@@ -9,9 +9,10 @@ every kind of byte position: element lengths 1..10 (zeros, field shares, full-ra
 either side of a tile, payloads at unaligned offsets, truncated final varints, jobs with elements of
 >= 6 bytes (the multi-round variant, slices longer than one word per lane), and moduli from 1 to
 i64::MAX (negative ones as |m|, as Rust's `%`).
-`SDA_CODEC_PATH=fused` selects it (it measured slower than the default decode-to-int32-matrix + combine,
-profiles/r02d/ab_codec_fused.txt, so it is opt-in); `=matrix` (or unset) is the default path.  Both must
-agree with the oracle on every case.
+`SDA_CODEC_PATH=fused` selects it (it measured slower, profiles/r02d/ab_codec_fused.txt, so it is opt-in);
+`=matrix` the count pass + dense int32 matrix + combine; `=slots` (or unset: the default) the single
+decode into int32 slots per 16 KiB region + the combine over the slots (round 3).  All three must agree
+with the oracle on every case; elements longer than 5 bytes send the slot path to the matrix path.
 """
 import numpy as np
 import pytest
@@ -70,8 +71,8 @@ def test_fused_decode_combine_shapes(engine, oracle, monkeypatch, kind, dim):
     x = _rows(rng, kind, n, dim)
     blobs = [oracle.varint_encode(r) for r in x]
     exp = oracle.combine(M31, x)
-    assert_same(_run(engine, M31, blobs, dim, "fused", monkeypatch), exp, f"{kind} fused")
-    assert_same(_run(engine, M31, blobs, dim, "matrix", monkeypatch), exp, f"{kind} matrix")
+    for path in ("fused", "matrix", "slots"):
+        assert_same(_run(engine, M31, blobs, dim, path, monkeypatch), exp, f"{kind} {path}")
 
 
 @pytest.mark.parametrize("m", [1, 2, 7, -M31, 2**31 + 11, 2**62 + 1, I64_MAX])
@@ -81,7 +82,8 @@ def test_fused_decode_combine_moduli(engine, oracle, monkeypatch, m):
     x = _rows(rng, "mixed", 6, 3001)
     x[0, :8] = [I64_MAX, I64_MAX, I64_MIN, -1, 0, 1, I64_MIN, I64_MAX]
     blobs = [oracle.varint_encode(r) for r in x]
-    assert_same(_run(engine, m, blobs, 3001, "fused", monkeypatch), oracle.combine(m, x))
+    for path in ("fused", "slots"):
+        assert_same(_run(engine, m, blobs, 3001, path, monkeypatch), oracle.combine(m, x), path)
 
 
 def test_fused_decode_combine_truncated_tails(engine, oracle, monkeypatch):
@@ -93,7 +95,8 @@ def test_fused_decode_combine_truncated_tails(engine, oracle, monkeypatch):
              for r in x]
     rows = np.stack([oracle.varint_decode(b) for b in blobs])
     assert rows.shape == (7, 2048)
-    assert_same(_run(engine, M31, blobs, 2048, "fused", monkeypatch), oracle.combine(M31, rows))
+    for path in ("fused", "slots"):
+        assert_same(_run(engine, M31, blobs, 2048, path, monkeypatch), oracle.combine(M31, rows), path)
 
 
 def test_fused_decode_combine_many_blobs_ragged_offsets(engine, oracle, monkeypatch):
@@ -105,8 +108,8 @@ def test_fused_decode_combine_many_blobs_ragged_offsets(engine, oracle, monkeypa
     x = x[rng.permutation(x.shape[0])]
     blobs = [oracle.varint_encode(r) for r in x]
     exp = oracle.combine(M31, x)
-    assert_same(_run(engine, M31, blobs, D, "fused", monkeypatch), exp)
-    assert_same(_run(engine, M31, blobs, D, "matrix", monkeypatch), exp)
+    for path in ("fused", "matrix", "slots"):
+        assert_same(_run(engine, M31, blobs, D, path, monkeypatch), exp, path)
 
 
 def test_fused_decode_combine_at_scale(engine, oracle, monkeypatch):
@@ -120,7 +123,7 @@ def test_fused_decode_combine_at_scale(engine, oracle, monkeypatch):
     row_bytes = engine.varint_encode_dev(x.data_ptr(), N, D, D, buf.data_ptr(), cap)
     off = np.concatenate([[0], np.cumsum(row_bytes)]).astype(np.uint64)
     exp = oracle.combine(M31, x.cpu().numpy())
-    for path in ("fused", "matrix"):
+    for path in ("fused", "matrix", "slots"):
         monkeypatch.setenv("SDA_CODEC_PATH", path)
         out = torch.full((D,), 7, dtype=torch.int64, device="cuda")
         assert engine.clerk_decode_combine_dev(M31, buf.data_ptr(), off, out.data_ptr(), D) == D
@@ -137,4 +140,21 @@ def test_fused_decode_combine_irregular_falls_back(engine, oracle, monkeypatch):
     blobs[2] = oracle.varint_encode(x[2][:-2]) + bytes([0xFF] * 12 + [0x01])   # 1498 + 2 elements
     rows = np.stack([oracle.varint_decode(b) for b in blobs])
     assert rows.shape == (4, 1500)
-    assert_same(_run(engine, M31, blobs, 1500, "fused", monkeypatch), oracle.combine(M31, rows))
+    for path in ("fused", "slots"):
+        assert_same(_run(engine, M31, blobs, 1500, path, monkeypatch), oracle.combine(M31, rows), path)
+
+
+@pytest.mark.parametrize("ones", [0, 1, 7, 3001, 8999])
+def test_slot_decode_combine_region_edges(engine, oracle, monkeypatch, ones):
+    """The slot path's tiles around 16 KiB region edges: the first payload mixes `ones` one-byte elements
+    with five-byte field shares, which moves every later payload's region boundaries, so tiles of 512
+    elements start near a region's end (or in a short first region) and continue in the next one."""
+    rng = np.random.default_rng(ones + 3)
+    D = 9_000
+    x = _rows(rng, "field", 12, D)
+    x[0, :ones] = 0
+    x[6] = 0                                                # a payload of 1-byte elements only
+    blobs = [oracle.varint_encode(r) for r in x]
+    exp = oracle.combine(M31, x)
+    for path in ("slots", "matrix"):
+        assert_same(_run(engine, M31, blobs, D, path, monkeypatch), exp, path)
