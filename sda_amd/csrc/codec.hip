@@ -30,6 +30,8 @@
 // sub-chunk per tile edge) and folds it into combiner.rs:16-28's exact recurrence in registers.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace sda {
@@ -415,76 +417,100 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
 // ---------------- the clerk's decode -> combine over region slots ----------------
 // After the SPARSE decode and varint_scan_kernel (region_base = the blob's elements before region r),
 // element j of blob b sits in the region r of b with region_base[r] <= j < region_base[r] + count[r],
-// at slot r * kRegionBytes + (j - region_base[r]).  The combine walks column tiles of kScTile elements:
-// plan[t * n_blobs + b] = r << 32 | (t * kScTile - region_base[r]), the region holding the tile's first
-// element.  One thread per (region, blob) emits the entries of the tiles whose first element it holds.
-constexpr uint32_t kScTile = 2 * kThreads;
+// at slot r * kRegionBytes + (j - region_base[r]).  The combine walks column tiles of `tile` elements.
+// A tile's elements lie in at most two regions: every element of this path has <= 5 bytes (any longer
+// one sets the wide flag and the job takes the matrix path), so a region the blob covers whole holds
+// >= kRegionBytes / 5 > tile elements, and a partial region is the blob's first or last.  The plan
+// entry of (tile t, blob b) is therefore self-contained -- no dependent load in the combine:
+//   bits  0..38  s0  = slot of the tile's first element (r * kRegionBytes + local offset)
+//   bits 39..49  c0  = min(elements of the tile in region r, tile)
+//   bits 50..63  gap = kRegionBytes - count[r]: element o >= c0 of the tile sits at s0 + o + gap
+// One thread per (region, blob) emits the entries of the tiles whose first element it holds.
+//
+// CPL columns per lane: lane l of a tile owns columns CPL*l .. CPL*l + CPL - 1 and reads them with one
+// CPL x 4-byte load per blob (tile = CPL x kThreads columns).  The slot index of a tile's first element
+// has no alignment, so the loads are only dword-aligned (global loads allow it).
+constexpr uint32_t kScMaxTile = 4 * kThreads;
+static_assert(kRegionBytes / 5 > kScMaxTile && kRegionBytes <= (1u << 14) && kScMaxTile < 2048, "slot plan packing");
+__device__ __forceinline__ uint64_t slot_plan_entry(uint64_t s0, uint64_t c0, uint64_t gap) {
+    return s0 | (c0 << 39) | (gap << 50);      // s0: 39 bits, c0: 11 bits, gap: 14 bits
+}
 __global__ __launch_bounds__(kThreads) void slot_plan_kernel(const uint64_t* __restrict__ blob_region,
                                                              const uint64_t* __restrict__ region_base,
                                                              const uint32_t* __restrict__ region_count, uint32_t y0,
-                                                             uint64_t n_blobs, uint64_t ntiles,
+                                                             uint64_t n_blobs, uint64_t ntiles, uint32_t tile,
                                                              uint64_t* __restrict__ plan) {
     const uint64_t b = y0 + blockIdx.y;
     const uint64_t r0 = blob_region[b], r1 = blob_region[b + 1];
     const uint64_t r = r0 + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (r >= r1) return;
-    const uint64_t E0 = region_base[r], E1 = E0 + region_count[r];
-    for (uint64_t t = (E0 + kScTile - 1) / kScTile; t < ntiles && t * kScTile < E1; ++t)
-        plan[t * n_blobs + b] = (r << 32) | (t * kScTile - E0);
+    const uint32_t cnt = region_count[r];
+    const uint64_t E0 = region_base[r], E1 = E0 + cnt;
+    const uint64_t gap = kRegionBytes - cnt;
+    for (uint64_t t = (E0 + tile - 1) / tile; t < ntiles && t * tile < E1; ++t) {
+        const uint64_t local = t * tile - E0;
+        const uint64_t c0 = E1 - t * tile < tile ? E1 - t * tile : tile;
+        plan[t * n_blobs + b] = slot_plan_entry(r * kRegionBytes + local, c0, gap);
+    }
 }
 
-// One workgroup per column tile: lane l owns columns e0 + l and e0 + 256 + l (each load instruction of a
-// wave reads 256 contiguous bytes of a region's slots) and walks the blobs in reference order through
-// combiner.rs:16-28's exact recurrence (add_trem).  A tile's elements lie in at most two regions unless a
-// blob's regions are tiny (then the lane walks on region by region).  Blobs go UNROLL at a time: their plan
-// entries and region counts are uniform (scalar loads), then all their slot loads are issued before the
-// dependent chain.  Every blob decoded to `dim` elements (checked on the host before the launch).
-template <int UNROLL>
+// One workgroup per column tile: lane l owns CPL adjacent columns and walks the blobs in reference order
+// through combiner.rs:16-28's exact recurrence (add_trem).  Blobs go UNROLL at a time: their plan entries
+// are uniform (scalar loads) and give every slot address directly, so all UNROLL slot loads are issued
+// before the dependent chain.  The one lane whose columns straddle the region boundary (c0) also loads
+// them past the gap and merges.  Every blob decoded to `dim` elements (checked on the host before the
+// launch); a lane's load may run past the blob's last element into unused slots (never past the buffer:
+// the tile plan follows the slots).
+template <int CPL, int UNROLL, bool SMALL_M>
 __global__ __launch_bounds__(kThreads) void slot_combine_kernel(const int32_t* __restrict__ slots,
                                                                 const uint64_t* __restrict__ plan,
-                                                                const uint32_t* __restrict__ region_count,
                                                                 uint64_t n_blobs, uint64_t dim,
-                                                                int64_t* __restrict__ out, Mod64 M, bool small_m) {
-    const uint64_t t = blockIdx.x;
-    const uint64_t e0 = t * kScTile;
-    const uint32_t o[2] = {threadIdx.x, threadIdx.x + kThreads};
-    const bool live[2] = {e0 + o[0] < dim, e0 + o[1] < dim};
-    const uint64_t* pl = plan + t * n_blobs;
-    auto slot_of = [&](uint64_t pe, uint32_t off) -> uint64_t {
-        uint64_t r = pe >> 32;
-        uint64_t local = (pe & 0xFFFFFFFFu) + off;
-        uint32_t c = region_count[r];
-        while (local >= c) {                     // the tile's tail lies in the blob's next region(s)
-            local -= c;
-            c = region_count[++r];
-        }
-        return r * kRegionBytes + local;
+                                                                int64_t* __restrict__ out, Mod64 M) {
+    typedef typename std::conditional<CPL == 1, int32_t,
+            int32_t __attribute__((ext_vector_type(CPL == 1 ? 2 : CPL)))>::type V;
+    constexpr uint32_t kTile = CPL * kThreads;
+    const uint64_t e0 = (uint64_t)blockIdx.x * kTile;
+    const uint32_t o = CPL * threadIdx.x;
+    if (e0 + o >= dim) return;
+    const uint64_t* pl = plan + (uint64_t)blockIdx.x * n_blobs;
+    auto get = [&](const V& v, int i) -> int32_t {
+        if constexpr (CPL == 1) return v; else return v[i];
     };
-    int64_t acc[2] = {0, 0};
+    auto load = [&](uint64_t pe) -> V {
+        const uint64_t s0 = pe & ((1ull << 39) - 1);
+        const uint32_t c0 = (uint32_t)(pe >> 39) & 2047u, gap = (uint32_t)(pe >> 50);
+        V v = __builtin_nontemporal_load(reinterpret_cast<const V*>(slots + s0 + o + (o >= c0 ? gap : 0u)));
+        if constexpr (CPL > 1) {
+            if (o < c0 && o + CPL > c0) {          // the lane straddling the region boundary
+                const V w = __builtin_nontemporal_load(reinterpret_cast<const V*>(slots + s0 + o + gap));
+#pragma unroll
+                for (int i = 0; i < CPL; ++i)
+                    if (o + i >= c0) v[i] = w[i];
+            }
+        }
+        return v;
+    };
+    int64_t acc[CPL];
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) acc[i] = 0;
     uint64_t b = 0;
     for (; b + UNROLL <= n_blobs; b += UNROLL) {
-        int32_t v[UNROLL][2];
+        V v[UNROLL];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const uint64_t pe = pl[b + u];
-#pragma unroll
-            for (int e = 0; e < 2; ++e)
-                v[u][e] = live[e] ? __builtin_nontemporal_load(slots + slot_of(pe, o[e])) : 0;
-        }
+        for (int u = 0; u < UNROLL; ++u) v[u] = load(pl[b + u]);
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-            for (int e = 0; e < 2; ++e) acc[e] = add_trem(acc[e], v[u][e], M, small_m);
+            for (int i = 0; i < CPL; ++i) acc[i] = add_trem(acc[i], get(v[u], i), M, SMALL_M);
     }
     for (; b < n_blobs; ++b) {
-        const uint64_t pe = pl[b];
+        const V v = load(pl[b]);
 #pragma unroll
-        for (int e = 0; e < 2; ++e)
-            if (live[e]) acc[e] = add_trem(acc[e], __builtin_nontemporal_load(slots + slot_of(pe, o[e])), M, small_m);
+        for (int i = 0; i < CPL; ++i) acc[i] = add_trem(acc[i], get(v, i), M, SMALL_M);
     }
 #pragma unroll
-    for (int e = 0; e < 2; ++e)
-        if (live[e]) out[e0 + o[e]] = acc[e];
+    for (int i = 0; i < CPL; ++i)
+        if (e0 + o + i < dim) out[e0 + o + i] = acc[i];
 }
 
 // ---------------- the clerk's fused decode -> combine ----------------
@@ -1066,8 +1092,15 @@ hipError_t launch_varint_decode_narrow(const uint8_t* bytes, uint64_t n_blobs, c
     return hipSuccess;
 }
 
+// Columns per lane of the slot combine (SDA_SLOT_CPL = 1, 2 or 4: A/B knob; default 4).
+static uint32_t slot_cpl() {
+    const char* e = getenv("SDA_SLOT_CPL");
+    const int v = e ? atoi(e) : 4;
+    return (v == 1 || v == 2) ? (uint32_t)v : 4u;
+}
+
 size_t varint_slot_bytes(const VarintPlan& plan, uint64_t n_blobs, uint64_t dim) {
-    const uint64_t ntiles = (dim + kScTile - 1) / kScTile;
+    const uint64_t ntiles = (dim + kThreads - 1) / kThreads;          // plan room for the smallest tile
     return plan.regions * kRegionBytes * sizeof(int32_t) + ntiles * n_blobs * 8 + 256;
 }
 
@@ -1107,20 +1140,25 @@ hipError_t launch_slot_combine(const VarintPlan& plan, void* work, const void* s
     const int32_t* slots = static_cast<const int32_t*>(slot_buf);
     uint64_t* tplan = reinterpret_cast<uint64_t*>(const_cast<char*>(static_cast<const char*>(slot_buf)) +
                                                   R * kRegionBytes * sizeof(int32_t));
-    const uint64_t ntiles = (dim + kScTile - 1) / kScTile;
-    if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t cpl = slot_cpl(), tile = cpl * kThreads;
+    const uint64_t ntiles = (dim + tile - 1) / tile;
+    if (ntiles > 0x7FFFFFFFull || R * kRegionBytes >= (1ull << 39)) return hipErrorInvalidValue;
     hipError_t e;
     for (uint64_t y0 = 0; y0 < n_blobs; y0 += 65535) {
         const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
         hipLaunchKernelGGL(slot_plan_kernel, dim3((unsigned)((plan.max_regions + kThreads - 1) / kThreads), ny),
                            dim3(kThreads), 0, s, w.blob_region, w.region_base, w.region_count, (uint32_t)y0, n_blobs,
-                           ntiles, tplan);
+                           ntiles, tile, tplan);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     const Mod64 M = make_mod64(modulus);
     const bool small_m = modulus <= ((int64_t)1 << 62);
-    hipLaunchKernelGGL(slot_combine_kernel<8>, dim3((unsigned)ntiles), dim3(kThreads), 0, s, slots, tplan,
-                       w.region_count, n_blobs, dim, out, M, small_m);
+    const dim3 g((unsigned)ntiles), blk(kThreads);
+#define SLOT_LAUNCH(C, SM) hipLaunchKernelGGL((slot_combine_kernel<C, 8, SM>), g, blk, 0, s, slots, tplan, n_blobs, dim, out, M)
+    if (cpl == 4) { if (small_m) SLOT_LAUNCH(4, true); else SLOT_LAUNCH(4, false); }
+    else if (cpl == 2) { if (small_m) SLOT_LAUNCH(2, true); else SLOT_LAUNCH(2, false); }
+    else { if (small_m) SLOT_LAUNCH(1, true); else SLOT_LAUNCH(1, false); }
+#undef SLOT_LAUNCH
     return hipGetLastError();
 }
 
