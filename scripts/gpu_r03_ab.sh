@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 A/B: exact share-gen with the sign-bit radix-2 half (default) vs the mad_i64 sign kernel
-# (SDA_GEN_SIGNBIT=0), interleaved, at 1000 and at 64 vectors per launch; then the HBM mix ceilings.
+# (SDA_GEN_SIGNBIT=0), interleaved, at 1000 and at 64 vectors per launch.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=gpurun_out/${1:-r03ab}
@@ -14,5 +14,5 @@ for r in 1 2 3; do
     done
   done
 done
-timeout -k 10 120 ./tools/ubench_mix > $T/ubench_mix.txt 2>&1 || exit 1
-cat $T/ubench_mix.txt
+
+

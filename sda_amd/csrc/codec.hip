@@ -42,6 +42,11 @@ constexpr int kThreads = 256;
 constexpr int kWPT = 4;                       // 16-byte words per thread: word t + 256 k, k < kWPT
 constexpr uint64_t kSubBytes = kThreads * 16; // one sub-region = one word per thread
 constexpr uint64_t kRegionBytes = kSubBytes * kWPT;
+// Slots per region of the clerk's slot decode: a region of 16 KiB holds at most 4096 elements of >= 4
+// bytes (a field share below 2^31 takes 4-5).  A region with more (short elements) raises *wide, and the
+// job takes the matrix path; the slot buffer has kRegionBytes - kSlotCap slots of slack at its end, so the
+// last region's overflowing stores stay inside it.
+constexpr uint64_t kSlotCap = 4096;
 
 
 
@@ -299,9 +304,9 @@ __device__ __forceinline__ int64_t varint_value_at(const uint32_t* lb, uint32_t 
 // narrowed and any value that does not fit sets *wide (the caller then decodes again as i64).
 //
 // SPARSE (the clerk's decode -> combine without a count pass): region r's elements go to its own slots
-// out + r * kRegionBytes (a region of kRegionBytes bytes holds at most that many elements), and the
-// region's element count to region_count[r]; region_base and blob_irregular are not read.  A malformed
-// blob (a run of >= 11 continuation bytes) always holds an element longer than 5 bytes, so it sets *wide.
+// out + r * kSlotCap, and the region's element count to region_count[r]; region_base and blob_irregular
+// are not read.  A region with more than kSlotCap elements sets *wide, and so does a malformed blob (a run
+// of >= 11 continuation bytes always holds an element longer than 5 bytes).
 template <typename OutT, bool SPARSE = false>
 __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* __restrict__ bytes,
                                                                  const uint64_t* __restrict__ blob_region,
@@ -337,7 +342,7 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
     uint4 h = make_uint4(0, 0, 0, 0);                         // the word before the region (thread 0)
     if (threadIdx.x == 0 && word * 16 > begin) h = p[word - 1];
     if (threadIdx.x == kThreads - 1) lb4[kThreads + 1] = make_uint4(0, 0, 0, 0);
-    OutT* dst = SPARSE ? out + r * kRegionBytes : out + (uint64_t)b * out_stride + region_base[r];
+    OutT* dst = SPARSE ? out + r * kSlotCap : out + (uint64_t)b * out_stride + region_base[r];
     bool narrow_fail = false;
     uint32_t base = 0;                                        // elements in earlier sub-regions
 #pragma unroll
@@ -410,28 +415,31 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
         if (narrow_fail) atomicOr(wide, 1u);             // rare: one atomic per lane that saw it
     }
     if constexpr (SPARSE) {
-        if (threadIdx.x == 0) region_count[r] = base;
+        if (threadIdx.x == 0) {
+            region_count[r] = base;
+            if (base > kSlotCap) atomicOr(wide, 1u);
+        }
     }
 }
 
 // ---------------- the clerk's decode -> combine over region slots ----------------
 // After the SPARSE decode and varint_scan_kernel (region_base = the blob's elements before region r),
 // element j of blob b sits in the region r of b with region_base[r] <= j < region_base[r] + count[r],
-// at slot r * kRegionBytes + (j - region_base[r]).  The combine walks column tiles of `tile` elements.
+// at slot r * kSlotCap + (j - region_base[r]).  The combine walks column tiles of `tile` elements.
 // A tile's elements lie in at most two regions: every element of this path has <= 5 bytes (any longer
 // one sets the wide flag and the job takes the matrix path), so a region the blob covers whole holds
 // >= kRegionBytes / 5 > tile elements, and a partial region is the blob's first or last.  The plan
 // entry of (tile t, blob b) is therefore self-contained -- no dependent load in the combine:
-//   bits  0..38  s0  = slot of the tile's first element (r * kRegionBytes + local offset)
+//   bits  0..38  s0  = slot of the tile's first element (r * kSlotCap + local offset)
 //   bits 39..49  c0  = min(elements of the tile in region r, tile)
-//   bits 50..63  gap = kRegionBytes - count[r]: element o >= c0 of the tile sits at s0 + o + gap
+//   bits 50..63  gap = kSlotCap - count[r]: element o >= c0 of the tile sits at s0 + o + gap
 // One thread per (region, blob) emits the entries of the tiles whose first element it holds.
 //
 // CPL columns per lane: lane l of a tile owns columns CPL*l .. CPL*l + CPL - 1 and reads them with one
 // CPL x 4-byte load per blob (tile = CPL x kThreads columns).  The slot index of a tile's first element
 // has no alignment, so the loads are only dword-aligned (global loads allow it).
 constexpr uint32_t kScMaxTile = 4 * kThreads;
-static_assert(kRegionBytes / 5 > kScMaxTile && kRegionBytes <= (1u << 14) && kScMaxTile < 2048, "slot plan packing");
+static_assert(kRegionBytes / 5 > kScMaxTile && kSlotCap <= (1u << 14) && kScMaxTile < 2048, "slot plan packing");
 __device__ __forceinline__ uint64_t slot_plan_entry(uint64_t s0, uint64_t c0, uint64_t gap) {
     return s0 | (c0 << 39) | (gap << 50);      // s0: 39 bits, c0: 11 bits, gap: 14 bits
 }
@@ -446,11 +454,11 @@ __global__ __launch_bounds__(kThreads) void slot_plan_kernel(const uint64_t* __r
     if (r >= r1) return;
     const uint32_t cnt = region_count[r];
     const uint64_t E0 = region_base[r], E1 = E0 + cnt;
-    const uint64_t gap = kRegionBytes - cnt;
+    const uint64_t gap = kSlotCap - cnt;
     for (uint64_t t = (E0 + tile - 1) / tile; t < ntiles && t * tile < E1; ++t) {
         const uint64_t local = t * tile - E0;
         const uint64_t c0 = E1 - t * tile < tile ? E1 - t * tile : tile;
-        plan[t * n_blobs + b] = slot_plan_entry(r * kRegionBytes + local, c0, gap);
+        plan[t * n_blobs + b] = slot_plan_entry(r * kSlotCap + local, c0, gap);
     }
 }
 
@@ -1101,7 +1109,7 @@ static uint32_t slot_cpl() {
 
 size_t varint_slot_bytes(const VarintPlan& plan, uint64_t n_blobs, uint64_t dim) {
     const uint64_t ntiles = (dim + kThreads - 1) / kThreads;          // plan room for the smallest tile
-    return plan.regions * kRegionBytes * sizeof(int32_t) + ntiles * n_blobs * 8 + 256;
+    return (plan.regions * kSlotCap + (kRegionBytes - kSlotCap)) * sizeof(int32_t) + ntiles * n_blobs * 8 + 256;
 }
 
 hipError_t launch_varint_decode_slots(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
@@ -1139,10 +1147,10 @@ hipError_t launch_slot_combine(const VarintPlan& plan, void* work, const void* s
     DecodeWork w = carve(work, R, n_blobs);
     const int32_t* slots = static_cast<const int32_t*>(slot_buf);
     uint64_t* tplan = reinterpret_cast<uint64_t*>(const_cast<char*>(static_cast<const char*>(slot_buf)) +
-                                                  R * kRegionBytes * sizeof(int32_t));
+                                                  (R * kSlotCap + (kRegionBytes - kSlotCap)) * sizeof(int32_t));
     const uint32_t cpl = slot_cpl(), tile = cpl * kThreads;
     const uint64_t ntiles = (dim + tile - 1) / tile;
-    if (ntiles > 0x7FFFFFFFull || R * kRegionBytes >= (1ull << 39)) return hipErrorInvalidValue;
+    if (ntiles > 0x7FFFFFFFull || R * kSlotCap >= (1ull << 39)) return hipErrorInvalidValue;
     hipError_t e;
     for (uint64_t y0 = 0; y0 < n_blobs; y0 += 65535) {
         const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);

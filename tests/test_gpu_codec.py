@@ -188,3 +188,35 @@ def test_continuation_runs_at_every_alignment(engine, oracle, monkeypatch, run):
         assert engine.clerk_decode_combine_dev(m, t.data_ptr(), off, res.data_ptr(), S) == S
         torch.cuda.synchronize()
         assert_same(res.cpu().numpy(), exp, f"{path} run={run}")
+
+
+@pytest.mark.parametrize("case", ["one_byte", "one_region", "exact_cap", "mixed_blobs"])
+def test_slot_cap_overflow_falls_back(engine, oracle, monkeypatch, case):
+    """The slot decode keeps 4096 slots per 16 KiB region (every element of >= 4 bytes fits); a region
+    with more elements (short ones) raises the wide flag and the job takes the matrix path.  Either way
+    the result is combiner.rs:16-28's exact one.  exact_cap: 4-byte elements fill a region to exactly
+    4096 (no fallback, gap 0)."""
+    rng = np.random.default_rng(77)
+    m = 2147482801
+    N, D = 6, 40_000
+    x = rng.integers(-(m - 1), m, size=(N, D), dtype=np.int64)
+    if case == "one_byte":                       # every element one byte: 16,384 per region
+        x = rng.integers(-64, 64, size=(N, D), dtype=np.int64)
+    elif case == "one_region":                   # a run of 9,000 one-byte elements inside a normal blob
+        x[2, 10_000:19_000] = rng.integers(-64, 64, size=9_000)
+    elif case == "exact_cap":                    # zigzag in [2^21, 2^28): 4 bytes each, blob 0 region-aligned
+        mag = rng.integers(2**20, 2**27, size=(N, D), dtype=np.int64)
+        x = np.where(rng.integers(0, 2, size=(N, D)) == 1, mag, -mag - 1)
+    else:                                        # blobs alternate between short and field-size elements
+        x[1::2] = rng.integers(-8000, 8000, size=(N // 2, D), dtype=np.int64)
+    blobs = [oracle.varint_encode(r) for r in x]
+    if case == "exact_cap":
+        assert all(len(b) == 4 * D for b in blobs)
+    t, off = _pack(blobs)
+    exp = oracle.combine(m, x)
+    for path in ("slots", "matrix"):
+        monkeypatch.setenv("SDA_CODEC_PATH", path)
+        res = torch.full((D,), 7, dtype=torch.int64, device="cuda")
+        assert engine.clerk_decode_combine_dev(m, t.data_ptr(), off, res.data_ptr(), D) == D
+        torch.cuda.synchronize()
+        assert_same(res.cpu().numpy(), exp, f"{case} {path}")
