@@ -51,6 +51,25 @@ def test_combine_dev_large(engine, oracle, dim, stride):
     assert (torch.remainder(col_sum, m).cpu().numpy() == np.mod(got, m)).all()
 
 
+def test_combine_dev_config1_full_size(engine, oracle):
+    """configs[1] at its own size on one GPU: 10,000 participations x 1M-dim (80 GB resident), signed
+    (-m, m) shares -- the order-dependent case.  1,024 sampled columns equal the oracle's sequential
+    recurrence bit for bit; every column's residue equals its int64 column sum mod m."""
+    m, N, D = 2147482801, 10_000, 1_000_000
+    x = torch.empty((N, D), dtype=torch.int64, device="cuda")
+    engine.synth_fill_dev(x.data_ptr(), N, D, 0x5DA + 31, -(m - 1), m, _stream())
+    out = torch.empty(D, dtype=torch.int64, device="cuda")
+    engine.combine_dev(m, x.data_ptr(), N, D, D, out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    cols = np.sort(np.random.default_rng(31).choice(D, 1024, replace=False))
+    xs = x[:, torch.from_numpy(cols).cuda()].cpu().numpy()
+    got = out.cpu().numpy()
+    assert_same(got[cols], oracle.combine(m, xs))
+    col_sum = x.sum(dim=0)                    # |sum| < N * m < 2^63
+    del x
+    assert torch.equal(torch.remainder(col_sum, m), torch.remainder(out, m))
+
+
 def test_combine_dev_canonical_and_finalize(engine):
     m, N, D = 2147482801, 512, 1_000_000
     x = torch.empty((N, D), dtype=torch.int64, device="cuda")
