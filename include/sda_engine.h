@@ -14,8 +14,11 @@
  *     return when results are in host memory), like the Rust trait calls.
  *   - Entry points suffixed `_dev` take DEVICE pointers and a hipStream_t
  *     (passed as void*; NULL = the HIP null stream, the same convention as the
- *     ROCm math libraries); they only enqueue work, except that the ChaCha
- *     combine waits for its rejection log (a few bytes) before returning.
+ *     ROCm math libraries); they only enqueue work, except for the few host
+ *     values they return: the ChaCha combine waits for its rejection log (a few
+ *     bytes) mid-call; the recipient and participant pipelines with ChaCha
+ *     masking, and the varint encode (row sizes), wait for their stream at the
+ *     end of the call instead, so no GPU idle gap opens inside them.
  *   - Randomness is explicit.  Where the reference draws from OsRng the caller
  *     passes the drawn values (or, for ChaCha masking, the seed words).
  *   - Every function returns an sda_status; 0 = OK.  The codes 1..6 map 1:1 to
@@ -296,7 +299,9 @@ sda_status sda_snapshot_transpose_dev(sda_engine* h, const uint8_t* src, const u
  *            (1..8 words); None = n_masks rows of width 0.
  *   shares [n_idx][share_len] at clerk `indices` (host array); dimension = the reconstructor's
  *   factory argument (vector_dimension); output_modulus = aggregation.modulus for positive().
- *   Errors as the reference: Not enough shares (6), Mismatching dimension (4), assert -> 64. */
+ *   Errors as the reference: Not enough shares (6), Mismatching dimension (4), assert -> 64.
+ *   With ChaCha masking the call drains its stream before returning: the mask's gen_range rejection
+ *   count is read then (the rare rejected draws are fixed and the unmask redone). */
 sda_status sda_recipient_reveal_dev(sda_engine* h, const sda_masking_scheme* ms, const void* mask_in,
                                     uint64_t n_masks, uint64_t mask_width, const sda_sharing_scheme* ss,
                                     uint64_t dimension, const uint64_t* indices, const int64_t* shares,
@@ -317,7 +322,9 @@ sda_status sda_recipient_reveal(sda_engine* h, const sda_masking_scheme* ms,
  * (Full); secrets [D], draws (as sda_share_generate) and shares_out [n][B] are device buffers.
  * mode: packed shares as tss' signed values (SDA_REVEAL_EXACT) or canonical residues
  * (SDA_REVEAL_CANONICAL, see sda_packed_generate_mode_dev); ignored for Additive.
- * payload (device, may be NULL): the n clerk payloads back to back, payload_row_bytes[n] (host). */
+ * payload (device, may be NULL): the n clerk payloads back to back, payload_row_bytes[n] (host).
+ * With ChaCha masking, or with payloads, the call drains its stream before returning (the mask's
+ * rejection count; the payload sizes). */
 sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms, const uint32_t* seed,
                                      uint64_t seed_words, const int64_t* full_masks,
                                      const sda_sharing_scheme* ss, const int64_t* secrets, uint64_t dimension,

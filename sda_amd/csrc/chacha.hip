@@ -73,10 +73,14 @@ struct RejectLog {
 // write-back is coalesced (lane t writes element t + 256 j): plain stores when the grid has a
 // single seed chunk (DIRECT: acc is the output), atomics into acc otherwise.
 constexpr int kChachaPad = 9;                  // LDS row stride (u64) of a lane's 8 results
-template <bool LAZY, bool DIRECT>
+// ADD (DIRECT, one stream: the participant's mask, chacha.rs:36-45): acc[e] = (secrets[e] + draw) % m
+// instead of the draw -- the mask itself is never stored.
+template <bool LAZY, bool DIRECT, bool ADD = false>
 __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __restrict__ seeds, uint32_t w, uint64_t n_seeds,
                            uint64_t seeds_per_chunk, uint64_t D, unsigned long long* __restrict__ acc, Mod64 M,
-                           uint64_t zone, uint64_t r64, RejectLog log) {
+                           uint64_t zone, uint64_t r64, RejectLog log,
+                           const int64_t* __restrict__ secrets = nullptr, bool small_m = false) {
+    static_assert(DIRECT || !ADD, "ADD needs the single-chunk grid");
     __shared__ unsigned long long st[256 * kChachaPad];
     const uint32_t tid = threadIdx.x;
     const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + tid;
@@ -134,7 +138,8 @@ __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __r
         const uint64_t e = e0 + idx;
         if (e < D) {
             const unsigned long long r = st[(idx >> 3) * kChachaPad + (idx & 7)];
-            if constexpr (DIRECT) acc[e] = r;
+            if constexpr (ADD) acc[e] = (unsigned long long)add_trem((int64_t)r, secrets[e], M, small_m);
+            else if constexpr (DIRECT) acc[e] = r;
             else atomicAdd(&acc[e], r);
         }
     }
@@ -397,9 +402,15 @@ hipError_t launch_chacha_stream(int64_t modulus, uint64_t D, const uint32_t* see
 }
 
 // ---- fast path (counter mode + rejection log) ----
-static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_t* seeds_dev, uint32_t w,
-                                      uint64_t n_seeds, int64_t* out, void* work, hipStream_t s, bool* overflow,
-                                      int* fixups_out) {
+// Split in two so a pipeline can keep queueing work behind the combine: chacha_fast_enqueue launches it
+// (canonical results land in `out`) and copies the rejection count to `count_host` (pinned); once the
+// stream has drained, chacha_fast_resolve applies the fix-ups for that count (rare: each draw is
+// rejected with probability < 2^-28 on this path) or reports a log overflow (the caller then runs the
+// stream path).
+// secrets != nullptr (one seed): out = (secrets + draw) % m, the masked secrets (ADD kernel).
+static hipError_t chacha_fast_enqueue(int64_t modulus, uint64_t D, const uint32_t* seeds_dev, uint32_t w,
+                                      uint64_t n_seeds, int64_t* out, void* work, hipStream_t s,
+                                      unsigned long long* count_host, const int64_t* secrets = nullptr) {
     const Mod64 M = make_mod64(modulus);
     const uint64_t zone = UINT64_MAX - UINT64_MAX % (uint64_t)modulus;
     char* base = static_cast<char*>(work);
@@ -407,7 +418,6 @@ static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_
     unsigned long long* count = reinterpret_cast<unsigned long long*>(base + D * 8);
     uint32_t* seed_of = reinterpret_cast<uint32_t*>(base + D * 8 + 16);
     uint64_t* pair_of = reinterpret_cast<uint64_t*>(base + D * 8 + 16 + kRejectCap * 4);
-    uint64_t* rej_up = pair_of + kRejectCap;
     hipError_t e;
     const uint64_t n_blk = (D + 7) / 8;
     const uint64_t gx = (n_blk + 255) / 256;
@@ -446,82 +456,93 @@ static hipError_t chacha_combine_fast(int64_t modulus, uint64_t D, const uint32_
         const uint64_t c = strtoull(ce, nullptr, 10);
         if (c >= 1 && c <= max_c) chunks = c;
     }
+    if (secrets) chunks = 1;                     // one stream: its own grid, no accumulator
     const uint64_t per = n_seeds ? (n_seeds + chunks - 1) / chunks : 0;
     const bool direct = chunks == 1;             // results stored straight into `out`
     unsigned long long* dst = direct ? reinterpret_cast<unsigned long long*>(out) : acc;
     if ((e = hipMemsetAsync(count, 0, 16, s)) != hipSuccess) return e;
     if (!direct && (e = hipMemsetAsync(acc, 0, D * 8, s)) != hipSuccess) return e;
     RejectLog log{count, seed_of, pair_of, kRejectCap};
-    {
-        const dim3 grid((unsigned)gx, (unsigned)chunks);
-        const uint64_t r64 = lazy ? (UINT64_MAX % mm + 1) % mm : 0;          // 2^64 mod m
+    const dim3 grid((unsigned)gx, (unsigned)chunks);
+    const uint64_t r64 = lazy ? (UINT64_MAX % mm + 1) % mm : 0;          // 2^64 mod m
 #define SDA_CHACHA_LAUNCH(L, DI)                                                                          \
     hipLaunchKernelGGL((chacha_combine_kernel<L, DI>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per, D, \
                        dst, M, zone, r64, log)
-        if (lazy && direct) SDA_CHACHA_LAUNCH(true, true);
-        else if (lazy) SDA_CHACHA_LAUNCH(true, false);
-        else if (direct) SDA_CHACHA_LAUNCH(false, true);
-        else SDA_CHACHA_LAUNCH(false, false);
+    const bool small_m = mm <= (1ull << 62);
+    if (secrets && lazy)
+        hipLaunchKernelGGL((chacha_combine_kernel<true, true, true>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds,
+                           per, D, dst, M, zone, r64, log, secrets, small_m);
+    else if (secrets)
+        hipLaunchKernelGGL((chacha_combine_kernel<false, true, true>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds,
+                           per, D, dst, M, zone, r64, log, secrets, small_m);
+    else if (lazy && direct) SDA_CHACHA_LAUNCH(true, true);
+    else if (lazy) SDA_CHACHA_LAUNCH(true, false);
+    else if (direct) SDA_CHACHA_LAUNCH(false, true);
+    else SDA_CHACHA_LAUNCH(false, false);
 #undef SDA_CHACHA_LAUNCH
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (!direct) {     // canonical residues into out (the fix-ups, if any, then work on out modulo m)
+        hipLaunchKernelGGL(acc_mod_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, acc, D, out, M);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        // read the rejection log (a few bytes) -- the call is synchronous anyway
-        unsigned long long n_rej = 0;
-        if ((e = hipMemcpyAsync(&n_rej, count, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        if (n_rej > kRejectCap) {          // the caller reruns the job on the stream path
+    }
+    return hipMemcpyAsync(count_host, count, 8, hipMemcpyDeviceToHost, s);
+}
+
+static hipError_t chacha_fast_resolve(int64_t modulus, uint64_t D, const uint32_t* seeds_dev, uint32_t w,
+                                      uint64_t n_seeds, int64_t* out, void* work, hipStream_t s,
+                                      unsigned long long n_rej, bool* overflow, int* fixups_out) {
+    if (n_rej == 0) return hipSuccess;
+    if (n_rej > kRejectCap) {          // the caller reruns the job on the stream path
+        *overflow = true;
+        return hipSuccess;
+    }
+    const Mod64 M = make_mod64(modulus);
+    const uint64_t zone = UINT64_MAX - UINT64_MAX % (uint64_t)modulus;
+    char* base = static_cast<char*>(work);
+    uint32_t* seed_of = reinterpret_cast<uint32_t*>(base + D * 8 + 16);
+    uint64_t* pair_of = reinterpret_cast<uint64_t*>(base + D * 8 + 16 + kRejectCap * 4);
+    uint64_t* rej_up = pair_of + kRejectCap;
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(out);   // canonical sums of the draws
+    hipError_t e;
+    std::vector<uint32_t> so(n_rej);
+    std::vector<uint64_t> po(n_rej);
+    std::vector<uint32_t> seeds_host((size_t)n_seeds * w);     // only now: keys of the affected streams
+    if ((e = hipMemcpy(so.data(), seed_of, n_rej * 4, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+    if ((e = hipMemcpy(po.data(), pair_of, n_rej * 8, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+    if ((e = hipMemcpy(seeds_host.data(), seeds_dev, seeds_host.size() * 4, hipMemcpyDeviceToHost)) != hipSuccess)
+        return e;
+    std::vector<std::pair<uint32_t, uint64_t>> ev(n_rej);
+    for (size_t i = 0; i < n_rej; ++i) ev[i] = {so[i], po[i]};
+    std::sort(ev.begin(), ev.end());
+    const uint32_t nw = w < 8 ? w : 8;
+    size_t i = 0;
+    while (i < ev.size()) {
+        const uint32_t sd = ev[i].first;
+        std::vector<uint64_t> rej;
+        while (i < ev.size() && ev[i].first == sd) rej.push_back(ev[i++].second);
+        Key8 key{};
+        for (uint32_t q = 0; q < nw; ++q) key.k[q] = seeds_host[(size_t)sd * w + q];
+        // extend past D: pairs D .. D + |rej| - 1 (+ any further rejections there)
+        uint64_t scanned = D;
+        while (scanned < D + rej.size()) {
+            const uint64_t v = h_pair(key.k, scanned);
+            if (v >= zone) rej.push_back(scanned);
+            ++scanned;
+        }
+        if (rej.size() > kRejectCap) {
             *overflow = true;
             return hipSuccess;
         }
-        if (n_rej) {
-            // canonicalise in place so the fix-ups can work modulo m without overflow (DIRECT: already)
-            if (!direct) {
-                hipLaunchKernelGGL(acc_mod_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, acc, D,
-                                   reinterpret_cast<int64_t*>(acc), M);
-                if ((e = hipGetLastError()) != hipSuccess) return e;
-            }
-            std::vector<uint32_t> so(n_rej);
-            std::vector<uint64_t> po(n_rej);
-            std::vector<uint32_t> seeds_host((size_t)n_seeds * w);     // only now: keys of the affected streams
-            if ((e = hipMemcpy(so.data(), seed_of, n_rej * 4, hipMemcpyDeviceToHost)) != hipSuccess) return e;
-            if ((e = hipMemcpy(po.data(), pair_of, n_rej * 8, hipMemcpyDeviceToHost)) != hipSuccess) return e;
-            if ((e = hipMemcpy(seeds_host.data(), seeds_dev, seeds_host.size() * 4, hipMemcpyDeviceToHost)) != hipSuccess)
-                return e;
-            std::vector<std::pair<uint32_t, uint64_t>> ev(n_rej);
-            for (size_t i = 0; i < n_rej; ++i) ev[i] = {so[i], po[i]};
-            std::sort(ev.begin(), ev.end());
-            const uint32_t nw = w < 8 ? w : 8;
-            size_t i = 0;
-            while (i < ev.size()) {
-                const uint32_t sd = ev[i].first;
-                std::vector<uint64_t> rej;
-                while (i < ev.size() && ev[i].first == sd) rej.push_back(ev[i++].second);
-                Key8 key{};
-                for (uint32_t q = 0; q < nw; ++q) key.k[q] = seeds_host[(size_t)sd * w + q];
-                // extend past D: pairs D .. D + |rej| - 1 (+ any further rejections there)
-                uint64_t scanned = D;
-                while (scanned < D + rej.size()) {
-                    const uint64_t v = h_pair(key.k, scanned);
-                    if (v >= zone) rej.push_back(scanned);
-                    ++scanned;
-                }
-                if (rej.size() > kRejectCap) {
-                    *overflow = true;
-                    return hipSuccess;
-                }
-                if ((e = hipMemcpy(rej_up, rej.data(), rej.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return e;
-                const uint64_t i0 = rej.front();
-                const uint64_t nfix = D - i0;
-                hipLaunchKernelGGL(chacha_fix_kernel, dim3((unsigned)((nfix + 255) / 256)), dim3(256), 0, s, key, i0, D,
-                                   rej_up, (uint32_t)rej.size(), dst, M);
-                if ((e = hipGetLastError()) != hipSuccess) return e;
-                if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;   // rej_up is reused
-                if (fixups_out) ++*fixups_out;
-            }
-        }
+        if ((e = hipMemcpy(rej_up, rej.data(), rej.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return e;
+        const uint64_t i0 = rej.front();
+        const uint64_t nfix = D - i0;
+        hipLaunchKernelGGL(chacha_fix_kernel, dim3((unsigned)((nfix + 255) / 256)), dim3(256), 0, s, key, i0, D,
+                           rej_up, (uint32_t)rej.size(), acc, M);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;   // rej_up is reused
+        if (fixups_out) ++*fixups_out;
     }
-    if (direct) return hipSuccess;
-    hipLaunchKernelGGL(acc_mod_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, acc, D, out, M);
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 hipError_t launch_chacha_mask_combine(int64_t modulus, uint64_t dimension, const uint32_t* seeds, uint32_t w,
@@ -530,7 +551,36 @@ hipError_t launch_chacha_mask_combine(int64_t modulus, uint64_t dimension, const
     *overflow = false;
     if (fixups_out) *fixups_out = 0;
     if (dimension == 0) return hipSuccess;
-    return chacha_combine_fast(modulus, dimension, seeds, w, n_seeds, out, work, s, overflow, fixups_out);
+    unsigned long long n_rej = 0;      // pageable: the copy completes before the sync returns
+    hipError_t e = chacha_fast_enqueue(modulus, dimension, seeds, w, n_seeds, out, work, s, &n_rej);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    return chacha_fast_resolve(modulus, dimension, seeds, w, n_seeds, out, work, s, n_rej, overflow, fixups_out);
+}
+
+hipError_t launch_chacha_mask_combine_async(int64_t modulus, uint64_t dimension, const uint32_t* seeds, uint32_t w,
+                                            uint64_t n_seeds, int64_t* out, void* work, hipStream_t s,
+                                            unsigned long long* count_host) {
+    *count_host = 0;
+    if (dimension == 0) return hipSuccess;
+    return chacha_fast_enqueue(modulus, dimension, seeds, w, n_seeds, out, work, s, count_host);
+}
+
+hipError_t launch_chacha_mask_add_async(int64_t modulus, uint64_t dimension, const uint32_t* seed, uint32_t w,
+                                        const int64_t* secrets, int64_t* masked, void* work, hipStream_t s,
+                                        unsigned long long* count_host) {
+    *count_host = 0;
+    if (dimension == 0) return hipSuccess;
+    return chacha_fast_enqueue(modulus, dimension, seed, w, 1, masked, work, s, count_host, secrets);
+}
+
+hipError_t resolve_chacha_mask_combine(int64_t modulus, uint64_t dimension, const uint32_t* seeds, uint32_t w,
+                                       uint64_t n_seeds, int64_t* out, void* work, hipStream_t s,
+                                       unsigned long long n_rej, bool* overflow, int* fixups_out) {
+    *overflow = false;
+    if (fixups_out) *fixups_out = 0;
+    if (dimension == 0) return hipSuccess;
+    return chacha_fast_resolve(modulus, dimension, seeds, w, n_seeds, out, work, s, n_rej, overflow, fixups_out);
 }
 
 }  // namespace sda

@@ -850,19 +850,23 @@ __device__ __forceinline__ uint64_t leb_spread8(uint64_t z) {
 // to their byte offset: 2-4 ds_or_b32, no per-byte stores), the image aligned to the chunk's global
 // byte offset mod 16 so that the interior leaves as 16-byte stores; the two partial 16-byte words at
 // the ends (shared with the neighbouring chunks) are written byte-wise.
-// chunk_off = row offset + exclusive scan of chunk_bytes.
+// Chunk (c, row) starts at dst + row_base[row] + chunk_off (the exclusive scan of the row's chunk_bytes);
+// nothing is written when *too_big (the rows do not fit dst_cap).
 __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* __restrict__ vals, uint64_t len,
                                                                 uint64_t stride, uint32_t chunks,
                                                                 const uint64_t* __restrict__ chunk_off,
+                                                                const uint64_t* __restrict__ row_base,
+                                                                const uint32_t* __restrict__ too_big,
                                                                 uint8_t* __restrict__ dst) {
     const uint32_t c = blockIdx.x, row = blockIdx.y;
+    if (*too_big) return;
     const uint64_t e0 = (uint64_t)c * kEncChunk;
     constexpr uint32_t kBufQuads = (kEncChunk * 10 + 32) / 16;      // lead < 16, + the shifted tail dwords
     __shared__ uint4 buf4[kBufQuads];
     __shared__ uint32_t wsum[kThreads / 64];
     uint32_t* buf = reinterpret_cast<uint32_t*>(buf4);
     const uint8_t* b8 = reinterpret_cast<const uint8_t*>(buf4);
-    uint8_t* gdst = dst + chunk_off[(uint64_t)row * chunks + c];
+    uint8_t* gdst = dst + row_base[row] + chunk_off[(uint64_t)row * chunks + c];
     const uint32_t lead = (uint32_t)((uintptr_t)gdst & 15);
     for (uint32_t k = threadIdx.x; k < kBufQuads; k += kThreads) buf4[k] = make_uint4(0, 0, 0, 0);
     // round q: lane t owns the kEncEpl adjacent elements e0 + R q + kEncEpl t + j (R = kEncEpl * 256;
@@ -950,6 +954,31 @@ __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* _
 }
 
 // exclusive scan of chunk_bytes per row (one block per row) + row base; row_bytes = total
+// One workgroup: rows placed back to back -- row_base = exclusive scan of row_bytes; *too_big = the total
+// exceeds cap (the write pass then writes nothing and the host reports it).
+__global__ __launch_bounds__(kThreads) void varint_rows_kernel(const uint64_t* __restrict__ row_bytes, uint64_t rows,
+                                                               uint64_t cap, uint64_t* __restrict__ row_base,
+                                                               uint32_t* __restrict__ too_big) {
+    __shared__ uint64_t part[kThreads];
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < rows; base += kThreads) {
+        const uint64_t r = base + threadIdx.x;
+        const uint64_t v = r < rows ? row_bytes[r] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < kThreads; o <<= 1) {
+            const uint64_t add = threadIdx.x >= (uint32_t)o ? part[threadIdx.x - o] : 0;
+            __syncthreads();
+            part[threadIdx.x] += add;
+            __syncthreads();
+        }
+        if (r < rows) row_base[r] = carry + part[threadIdx.x] - v;
+        carry += part[kThreads - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *too_big = carry > cap ? 1u : 0u;
+}
+
 __global__ __launch_bounds__(kThreads) void varint_offsets_kernel(const uint64_t* __restrict__ chunk_bytes,
                                                                   uint32_t chunks, const uint64_t* __restrict__ row_base,
                                                                   uint64_t* __restrict__ chunk_off,
@@ -1209,7 +1238,7 @@ hipError_t launch_varint_decode_combine(const uint8_t* bytes, uint64_t n_blobs, 
 
 size_t varint_encode_work_bytes(uint64_t rows, uint64_t len) {
     const uint64_t chunks = (len + kEncChunk - 1) / kEncChunk;
-    return 2 * rows * (chunks ? chunks : 1) * 8 + 2 * rows * 8 + 1024;
+    return 2 * rows * (chunks ? chunks : 1) * 8 + 2 * rows * 8 + 1024 + 256;
 }
 
 hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len, uint64_t stride, uint8_t* dst,
@@ -1220,6 +1249,7 @@ hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len
     uint64_t* chunk_off = chunk_bytes + rows * (chunks ? chunks : 1);
     uint64_t* row_base = chunk_off + rows * (chunks ? chunks : 1);
     uint64_t* rbytes = row_base + rows;
+    uint32_t* too_big = reinterpret_cast<uint32_t*>(rbytes + rows);
     hipError_t e;
     if (chunks == 0) {
         for (uint64_t r = 0; r < rows; ++r) row_bytes_host[r] = 0;
@@ -1228,23 +1258,23 @@ hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len
     hipLaunchKernelGGL(varint_size_kernel, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s, vals, len,
                        stride, (uint32_t)chunks, chunk_bytes);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    // per-row totals first (row_base = nullptr), then the host places rows back to back
+    // per row: its chunks' offsets and its total; then the rows back to back -- all on the device, so the
+    // only host wait is the row sizes' copy at the end
     hipLaunchKernelGGL(varint_offsets_kernel, dim3((unsigned)rows), dim3(kThreads), 0, s, chunk_bytes,
                        (uint32_t)chunks, (const uint64_t*)nullptr, chunk_off, rbytes);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(row_bytes_host, rbytes, rows * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    std::vector<uint64_t> base(rows);
-    uint64_t acc = 0;
-    for (uint64_t r = 0; r < rows; ++r) { base[r] = acc; acc += row_bytes_host[r]; }
-    if (acc > dst_cap) return hipErrorInvalidValue;
-    if ((e = hipMemcpyAsync(row_base, base.data(), rows * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(varint_offsets_kernel, dim3((unsigned)rows), dim3(kThreads), 0, s, chunk_bytes,
-                       (uint32_t)chunks, (const uint64_t*)row_base, chunk_off, (uint64_t*)nullptr);
+    hipLaunchKernelGGL(varint_rows_kernel, dim3(1), dim3(kThreads), 0, s, (const uint64_t*)rbytes, rows, dst_cap,
+                       row_base, too_big);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(varint_write_kernel, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s, vals, len,
-                       stride, (uint32_t)chunks, chunk_off, dst);
-    return hipGetLastError();
+                       stride, (uint32_t)chunks, (const uint64_t*)chunk_off, (const uint64_t*)row_base,
+                       (const uint32_t*)too_big, dst);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(row_bytes_host, rbytes, rows * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    uint64_t acc = 0;
+    for (uint64_t r = 0; r < rows; ++r) acc += row_bytes_host[r];
+    return acc > dst_cap ? hipErrorInvalidValue : hipSuccess;     // nothing was written (too_big)
 }
 
 }  // namespace sda

@@ -41,6 +41,7 @@ struct sda_engine {
     // than the previous one first waits (on the device) for the work queued on that stream.
     hipStream_t last_stream = nullptr;
     hipEvent_t order_ev = nullptr;
+    unsigned long long* rej_host = nullptr;   // pinned: the ChaCha rejection count of a pipeline's mask
 };
 
 namespace {
@@ -204,6 +205,44 @@ sda_status chacha_combine(sda_engine* h, int64_t m, uint64_t D, const uint32_t* 
     return SDA_OK;
 }
 
+// chacha_combine for a pipeline that keeps queueing work behind the mask: the rejection count is copied
+// to the handle's pinned word instead of being waited for, and chacha_combine_end -- called after the
+// pipeline's own final stream sync -- applies the fix-ups (each draw is rejected with probability
+// < 2^-28 on this path, so a call rarely has any).  *changed tells the caller to redo what it queued on
+// `out`.  Moduli that need the stream path run it synchronously in _begin, as chacha_combine does.
+struct PendingChacha {
+    bool pending = false;
+    int64_t m = 0;
+    uint64_t D = 0, n = 0;
+    const uint32_t* seeds = nullptr;
+    uint32_t w = 0;
+    int64_t* out = nullptr;
+};
+sda_status chacha_combine_begin(sda_engine* h, int64_t m, uint64_t D, const uint32_t* seeds, uint32_t w, uint64_t n,
+                                int64_t* out, hipStream_t st, PendingChacha* pc) {
+    *pc = PendingChacha{};
+    if (D == 0) return SDA_OK;
+    const char* force = getenv("SDA_CHACHA_PATH");
+    if (sda::chacha_needs_stream_path(m) || (force && strcmp(force, "stream") == 0) || n == 0)
+        return chacha_combine(h, m, D, seeds, w, n, out, st);
+    if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D))) return e;
+    HIP_TRY(sda::launch_chacha_mask_combine_async(m, D, seeds, w, n, out, h->work, st, h->rej_host));
+    *pc = PendingChacha{true, m, D, n, seeds, w, out};
+    return SDA_OK;
+}
+sda_status chacha_combine_end(sda_engine* h, const PendingChacha& pc, hipStream_t st, bool* changed) {
+    *changed = false;
+    if (!pc.pending || *h->rej_host == 0) return SDA_OK;
+    *changed = true;
+    bool overflow = false;
+    HIP_TRY(sda::resolve_chacha_mask_combine(pc.m, pc.D, pc.seeds, pc.w, pc.n, pc.out, h->work, st, *h->rej_host,
+                                             &overflow, nullptr));
+    if (!overflow) return SDA_OK;
+    if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_stream_work_bytes(pc.D, pc.n, pc.m))) return e;
+    HIP_TRY(sda::launch_chacha_streams_combine(pc.m, pc.D, pc.seeds, pc.w, pc.n, pc.out, h->work, st));
+    return SDA_OK;
+}
+
 // chacha.rs:36-45: masked = (secrets + draw) % m for one seed (host words); mask = scratch of D values
 sda_status chacha_mask(sda_engine* h, int64_t m, const uint32_t* seed_host, uint32_t w, const int64_t* secrets,
                        uint64_t D, int64_t* mask, uint32_t* seed_dev, int64_t* masked, hipStream_t st) {
@@ -257,7 +296,9 @@ sda_status sda_engine_create(int device_ordinal, sda_engine** out) {
     h->device = device_ordinal;
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&h->rej_host), 64, hipHostMallocDefault);
     if (e != hipSuccess) {
+        if (h->order_ev) (void)hipEventDestroy(h->order_ev);
         if (h->stream) (void)hipStreamDestroy(h->stream);
         delete h;
         return fail(SDA_ERR_DEVICE, "hipStreamCreate/hipEventCreate: %s", hipGetErrorString(e));
@@ -281,6 +322,7 @@ void sda_engine_destroy(sda_engine* h) {
     if (h->stage) (void)hipFree(h->stage);
     sda::free_table(h->gen_tab);
     sda::free_table(h->rev_tab);
+    if (h->rej_host) (void)hipHostFree(h->rej_host);
     if (h->order_ev) (void)hipEventDestroy(h->order_ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -1137,9 +1179,11 @@ sda_status recipient_pipeline(sda_engine* h, const sda_masking_scheme* ms, const
     if (ms->kind == SDA_MASKING_FULL) {
         if (sda_status e = modulus_abs(ms->modulus, &q)) return e;
         HIP_TRY(sda::launch_combine_exact(static_cast<const int64_t*>(mask_in), n_masks, D, mask_width, dmask, q, st));
-    } else if (ms->kind == SDA_MASKING_CHACHA) {
-        if (sda_status e = chacha_combine(h, ms->modulus, D, static_cast<const uint32_t*>(mask_in),
-                                          (uint32_t)mask_width, n_masks, dmask, st))
+    }
+    PendingChacha pc;                                       // ChaCha: its rejection count is checked at the end
+    if (ms->kind == SDA_MASKING_CHACHA) {
+        if (sda_status e = chacha_combine_begin(h, ms->modulus, D, static_cast<const uint32_t*>(mask_in),
+                                                (uint32_t)mask_width, n_masks, dmask, st, &pc))
             return e;
     }
     // 2. reconstruct (receive.rs:120-146)
@@ -1166,6 +1210,13 @@ sda_status recipient_pipeline(sda_engine* h, const sda_masking_scheme* ms, const
     // 3. unmask (receive.rs:149-152) + RecipientOutput::positive (:14-20), one pass
     HIP_TRY(sda::launch_unmask_positive(dmasked, ms->kind == SDA_MASKING_NONE ? nullptr : dmask, D, q,
                                         output_modulus, out, st));
+    if (pc.pending) {            // the mask's rejection count: fix the mask and unmask again if it had any
+        HIP_TRY(hipStreamSynchronize(st));
+        bool changed = false;
+        if (sda_status e = chacha_combine_end(h, pc, st, &changed)) return e;
+        if (changed)
+            HIP_TRY(sda::launch_unmask_positive(dmasked, dmask, D, q, output_modulus, out, st));
+    }
     *out_len = D;
     return SDA_OK;
 }
@@ -1269,6 +1320,13 @@ sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms
     }
     // 1. SecretMasker::mask (participate.rs:53-54)
     const int64_t* masked = secrets;
+    // ChaCha on the fast path: the masked secrets come straight out of the ChaCha kernel and its rejection
+    // count is checked at the end of the call (a nonzero count -- probability < 2^-28 per draw -- redoes
+    // the mask exactly, then every later step)
+    bool mask_pending = false;
+    int64_t* cmask = nullptr;
+    uint32_t* cseed = nullptr;
+    uint32_t cw = 0;
     if (ms->kind != SDA_MASKING_NONE && D) {
         if (ms->modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
         if (sda_status e = ensure(&h->pipe, &h->pipe_bytes, 2 * rup(D * 8) + 256)) return e;
@@ -1283,9 +1341,22 @@ sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms
                 return fail(SDA_ERR_PRECONDITION, "expected %llu seed words", (unsigned long long)want);
             int64_t* dmask = dm + rup(D * 8) / 8;
             uint32_t* dseed = reinterpret_cast<uint32_t*>(dmask + rup(D * 8) / 8);
-            if (sda_status e = chacha_mask(h, ms->modulus, seed, (uint32_t)(seed_words < 8 ? seed_words : 8), secrets,
-                                           D, dmask, dseed, dm, st))                                 // chacha.rs:36-45
-                return e;
+            const uint32_t w = (uint32_t)(seed_words < 8 ? seed_words : 8);
+            if (w) HIP_TRY(hipMemcpyAsync(dseed, seed, w * 4, hipMemcpyHostToDevice, st));
+            // chacha.rs:36-45: masked = (secrets + draw) % m over one stream
+            const char* force = getenv("SDA_CHACHA_PATH");
+            if (!sda::chacha_needs_stream_path(ms->modulus) && !(force && strcmp(force, "stream") == 0)) {
+                if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D))) return e;
+                HIP_TRY(sda::launch_chacha_mask_add_async(ms->modulus, D, dseed, w, secrets, dm, h->work, st,
+                                                          h->rej_host));
+                mask_pending = true;
+            } else {
+                if (sda_status e = chacha_combine(h, ms->modulus, D, dseed, w, 1, dmask, st)) return e;
+                HIP_TRY(sda::launch_addsub_trem(secrets, dmask, +1, D, dm, ms->modulus, st));
+            }
+            cmask = dmask;
+            cseed = dseed;
+            cw = w;
         } else {
             return fail(SDA_ERR_INVALID_ARGUMENT, "unknown masking scheme kind");
         }
@@ -1294,26 +1365,39 @@ sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms
     // 2. ShareGenerator::generate (participate.rs:75-76): shares [n][B]
     const uint64_t n = ss->share_count;
     const uint64_t B = packed ? (D + ss->secret_count - 1) / ss->secret_count : D;
-    if (B) {
-        if (!draws) return fail(SDA_ERR_INVALID_ARGUMENT, "need the randomness draws");
-        if (packed) {
-            if (sda_status e = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return e;
-            sda::PackedGenArgs ga{masked, D, 1, draws, shares_out, mode == SDA_REVEAL_CANONICAL};
-            HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)ss->secret_count, (uint32_t)ss->privacy_threshold,
-                                                (uint32_t)n, (uint32_t)ss->modulus, (uint32_t)ss->omega_secrets,
-                                                (uint32_t)ss->omega_shares, h->gen_tab, h->gen_log, st));
-        } else {
-            HIP_TRY(sda::launch_additive_generate(masked, D, draws, n, shares_out, ss->modulus, st));
+    if (B && !draws) return fail(SDA_ERR_INVALID_ARGUMENT, "need the randomness draws");
+    if (payload && n > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 clerks");
+    auto share_and_encode = [&]() -> sda_status {
+        if (B) {
+            if (packed) {
+                if (sda_status e = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return e;
+                sda::PackedGenArgs ga{masked, D, 1, draws, shares_out, mode == SDA_REVEAL_CANONICAL};
+                HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)ss->secret_count, (uint32_t)ss->privacy_threshold,
+                                                    (uint32_t)n, (uint32_t)ss->modulus, (uint32_t)ss->omega_secrets,
+                                                    (uint32_t)ss->omega_shares, h->gen_tab, h->gen_log, st));
+            } else {
+                HIP_TRY(sda::launch_additive_generate(masked, D, draws, n, shares_out, ss->modulus, st));
+            }
         }
-    }
-    // 3. per-clerk payload encoding (participate.rs:79-98 -> sodium.rs:36-41); sealing stays on the host
-    if (payload) {
-        if (n > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 clerks");
-        if (sda_status e = ensure(&h->codec_work, &h->codec_work_bytes, sda::varint_encode_work_bytes(n, B))) return e;
-        hipError_t e = sda::launch_varint_encode(shares_out, n, B, B, payload, payload_cap, h->codec_work,
-                                                 payload_row_bytes, st);
-        if (e == hipErrorInvalidValue) return fail(SDA_ERR_INVALID_ARGUMENT, "payload_cap too small");
-        HIP_TRY(e);
+        // 3. per-clerk payload encoding (participate.rs:79-98 -> sodium.rs:36-41); sealing stays on the host
+        if (payload) {
+            if (sda_status e = ensure(&h->codec_work, &h->codec_work_bytes, sda::varint_encode_work_bytes(n, B)))
+                return e;
+            hipError_t e = sda::launch_varint_encode(shares_out, n, B, B, payload, payload_cap, h->codec_work,
+                                                     payload_row_bytes, st);
+            if (e == hipErrorInvalidValue) return fail(SDA_ERR_INVALID_ARGUMENT, "payload_cap too small");
+            HIP_TRY(e);
+        }
+        return SDA_OK;
+    };
+    if (sda_status e = share_and_encode()) return e;
+    if (mask_pending) {          // the mask's rejection count: redo the mask exactly, and every later step
+        HIP_TRY(hipStreamSynchronize(st));
+        if (*h->rej_host) {
+            if (sda_status e = chacha_combine(h, ms->modulus, D, cseed, cw, 1, cmask, st)) return e;
+            HIP_TRY(sda::launch_addsub_trem(secrets, cmask, +1, D, const_cast<int64_t*>(masked), ms->modulus, st));
+            if (sda_status e = share_and_encode()) return e;
+        }
     }
     return ok();
 }

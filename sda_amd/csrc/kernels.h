@@ -167,6 +167,23 @@ size_t chacha_stream_work_bytes(uint64_t dimension, uint64_t n_seeds, int64_t mo
 hipError_t launch_chacha_mask_combine(int64_t modulus, uint64_t dimension, const uint32_t* seeds,
                                       uint32_t w, uint64_t n_seeds, int64_t* out, void* work,
                                       hipStream_t s, bool* overflow, int* fixups_out);
+// The same fast path in two halves, for pipelines that keep queueing work behind it: _async enqueues
+// the combine (canonical draws' sums in out, before any fix-up) and copies its rejection count to
+// count_host (PINNED host memory, valid once the stream has drained); resolve_ then applies the
+// fix-ups for that count (host-synchronous, rare) or sets *overflow (rerun on the stream path).  The
+// caller redoes whatever it queued on `out` when the count was nonzero.
+hipError_t launch_chacha_mask_combine_async(int64_t modulus, uint64_t dimension, const uint32_t* seeds, uint32_t w,
+                                            uint64_t n_seeds, int64_t* out, void* work, hipStream_t s,
+                                            unsigned long long* count_host);
+// One stream's masked secrets in one pass (chacha.rs:36-45): masked = (secrets + draw) % m, the rejection
+// count to count_host (pinned).  A nonzero count means `masked` used rejected draws: the caller redoes
+// the mask exactly (launch_chacha_mask_combine, then the add).
+hipError_t launch_chacha_mask_add_async(int64_t modulus, uint64_t dimension, const uint32_t* seed, uint32_t w,
+                                        const int64_t* secrets, int64_t* masked, void* work, hipStream_t s,
+                                        unsigned long long* count_host);
+hipError_t resolve_chacha_mask_combine(int64_t modulus, uint64_t dimension, const uint32_t* seeds, uint32_t w,
+                                       uint64_t n_seeds, int64_t* out, void* work, hipStream_t s,
+                                       unsigned long long n_rej, bool* overflow, int* fixups_out);
 hipError_t launch_chacha_streams_combine(int64_t modulus, uint64_t dimension, const uint32_t* seeds, uint32_t w,
                                          uint64_t n_seeds, int64_t* out, void* work, hipStream_t s);
 // mask[i] = gen_range draw i of one stream (chacha.rs:36-39); `work`: chacha_stream_work_bytes(D, 1, m)

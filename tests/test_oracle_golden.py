@@ -212,3 +212,17 @@ def test_varint_codec(oracle):
     enc = oracle.varint_encode(vals)
     assert enc[:3] == bytes([0, 1, 2])          # zigzag: 0 -> 0, -1 -> 1, 1 -> 2
     assert oracle.varint_decode(enc).tolist() == vals.tolist()
+
+
+def test_chacha_reject_seeds_reject_where_found(oracle):
+    """tests/golden/chacha_rejects.json (the GPU search of tools/chacha_reject_search.hip): the oracle's
+    rand-0.3 stream of every listed seed rejects a draw (v >= u64::MAX - u64::MAX % m) exactly at the
+    reported pair and at no earlier one -- so the rejection tests' inputs really exercise the fix-up."""
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "chacha_rejects.json")))
+    for m, hits in g["moduli"].items():
+        m = int(m)
+        zone = (2**64 - 1) - (2**64 - 1) % m
+        assert len(hits) >= 5
+        for s, pair in hits:
+            r = oracle.Rng([s, 0x5DA, 7, 11])
+            assert [i for i in range(pair + 1) if r.next_u64() >= zone] == [pair]
