@@ -526,77 +526,83 @@ template hipError_t gen_dispatch_L<SDA_GEN_PART>(uint32_t, const PackedGenArgs&,
 
 namespace {
 
-// ---------------- generic exact share (inputs outside (-p, p)) ----------------
-// Reads its inputs from global memory (nothing escapes from the fast path's registers).
-__device__ __noinline__ void packed_share_generic(const int64_t* __restrict__ sec, uint64_t D,
-                                                  const int64_t* __restrict__ drw, uint64_t b, uint32_t k,
-                                                  int L, int N3, const GenTables& T, int64_t* o, uint64_t B) {
-    const Mod64 P = make_mod64((int64_t)T.M.p);
-    int64_t x[64];
-    const int lb = ilog(L, 2);
-    for (int i = 0; i < L; ++i) {
-        int r = 0, v = i;
-        for (int d = 0; d < lb; ++d) { r = r * 2 + v % 2; v /= 2; }
-        int64_t val = 0;
-        if (i >= 1 && (uint32_t)i <= k) { const uint64_t idx = b * k + (i - 1); val = idx < D ? sec[idx] : 0; }
-        else if (i > 0) val = drw[i - 1 - k];
-        x[r] = val;
-    }
-    for (int len = 2; len <= L; len *= 2) {
-        const int h = len / 2;
-        for (int g = 0; g < L; g += len)
-            for (int i = 0; i < h; ++i) {
-                const int64_t w = T.tw2[h - 1 + i];
-                const int64_t u = x[g + i], c = x[g + i + h];
-                x[g + i] = trem64(wadd(u, wmul(w, c)), P);
-                x[g + i + h] = trem64(wsub(u, wmul(w, c)), P);
-            }
-    }
-    for (int i = 0; i < L; ++i) x[i] = trem64(wmul(x[i], T.linv), P);
-    int64_t y[81];
-    const int nd = ilog(N3, 3);
-    for (int i = 0; i < N3; ++i) {
-        int r = 0, v = i;
-        for (int d = 0; d < nd; ++d) { r = r * 3 + v % 3; v /= 3; }
-        y[r] = i < L ? x[i] : 0;
-    }
-    for (int len = 3; len <= N3; len *= 3) {
-        const int th = len / 3, o = (len - 3) / 2;
-        for (int g = 0; g < N3; g += len)
-            for (int i = 0; i < th; ++i) {
-                const int64_t b = y[g + i], c = y[g + i + th], d = y[g + i + 2 * th];
-                for (int q = 0; q < 3; ++q) {
-                    const int j = i + q * th;
-                    y[g + j] = trem64(wadd(wadd(b, wmul(T.tw3[o + j], c)), wmul(T.sq3[o + j], d)), P);
-                }
-            }
-    }
-    for (int j = 1; j < N3; ++j) o[(uint64_t)(j - 1) * B] = y[j];
-}
-
-// Batches the fast kernel logged (inputs outside (-p, p)), recomputed with the generic exact path.
-// If the log overflowed, every batch of the launch is recomputed (correct, slow, and only
-// reachable with raw i64 secrets far outside the field).
-__global__ __launch_bounds__(256) void packed_gen_fixup_kernel(const int64_t* __restrict__ secrets, uint64_t D,
-                                                               const int64_t* __restrict__ draws,
-                                                               int64_t* __restrict__ out, uint32_t k, uint32_t t,
-                                                               uint64_t B, uint64_t n_vec, int L, int N3,
-                                                               const GenTables* __restrict__ T, GenFixupLog log,
-                                                               int canonical) {
+// ---------------- generic exact share-gen fix-up ----------------
+// Batches the fast kernel logged -- inputs outside (-p, p) (raw i64 secrets), or a lazy-truncation /
+// sign-bit trap -- recomputed with tss' operations verbatim: wrapping i64 products and sums, Rust's
+// truncated % after every butterfly, the fast kernels' tables.  One wave per batch (the transform is the
+// same one lane's generic path used to run serially, ~55 us per launch): lane j takes butterfly j of a
+// radix-2 level and outputs j, j + 64 of a radix-3 level, the state in LDS (radix-3 levels double
+// buffered, as their outputs overwrite other lanes' inputs).  If the log overflowed, every batch of the
+// launch is recomputed (correct, slow, and only reachable with raw i64 secrets far outside the field).
+__global__ __launch_bounds__(64) void packed_gen_fixup_kernel(const int64_t* __restrict__ secrets, uint64_t D,
+                                                              const int64_t* __restrict__ draws,
+                                                              int64_t* __restrict__ out, uint32_t k, uint32_t t,
+                                                              uint64_t B, uint64_t n_vec, int L, int N3,
+                                                              const GenTables* __restrict__ T, GenFixupLog log,
+                                                              int canonical) {
     const uint32_t n = *log.count;
     if (n == 0) return;
     const bool all = n > log.cap;
     const uint64_t total = all ? B * n_vec : (uint64_t)n;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+    __shared__ int64_t xa[64];
+    __shared__ int64_t ya[2][81];
+    const Mod64 P = make_mod64((int64_t)T->M.p);
+    const int lane = threadIdx.x;
+    const int lb = ilog(L, 2), nd = ilog(N3, 3);
+    for (uint64_t i = blockIdx.x; i < total; i += gridDim.x) {
         const uint64_t gb = all ? i : log.list[i];
         const uint64_t vec = gb / B, b = gb - vec * B;
-        int64_t* o = out + vec * (uint64_t)(N3 - 1) * B + b;
-        packed_share_generic(secrets + vec * D, D, draws + gb * t, b, k, L, N3, *T, o, B);
-        if (canonical)                      // the exact share's canonical residue
-            for (int j = 1; j < N3; ++j) {
-                const int64_t v = o[(uint64_t)(j - 1) * B];
-                o[(uint64_t)(j - 1) * B] = v < 0 ? v + (int64_t)T->M.p : v;
+        __syncthreads();                                 // the previous batch's stores have read ya
+        // values = [0, secrets (zero past D: batched.rs:37-43), randomness], bit-reversed
+        if (lane < L) {
+            int64_t val = 0;
+            if (lane >= 1 && (uint32_t)lane <= k) {
+                const uint64_t idx = b * k + (lane - 1);
+                val = idx < D ? secrets[vec * D + idx] : 0;
+            } else if (lane > 0) {
+                val = draws[gb * t + (lane - 1 - k)];
             }
+            xa[rev_digits(lane, 2, lb)] = val;
+        }
+        // fft2_inverse: butterfly `lane` of each level, (u +- w c) % p
+        for (int len = 2; len <= L; len *= 2) {
+            const int h = len / 2, g = (lane / h) * len, ii = lane % h;
+            __syncthreads();
+            int64_t u = 0, c = 0, w = 0;
+            if (lane < L / 2) {
+                u = xa[g + ii];
+                c = xa[g + ii + h];
+                w = T->tw2[h - 1 + ii];
+            }
+            __syncthreads();
+            if (lane < L / 2) {
+                xa[g + ii] = trem64(wadd(u, wmul(w, c)), P);
+                xa[g + ii + h] = trem64(wsub(u, wmul(w, c)), P);
+            }
+        }
+        __syncthreads();
+        // x * len_inv % p, zero-extended to N3 and digit-reversed
+        for (int j = lane; j < N3; j += 64)
+            ya[0][rev_digits(j, 3, nd)] = j < L ? trem64(wmul(xa[j], (int64_t)T->linv), P) : 0;
+        // fft3: output j of each level, (b + x c + x^2 d) % p
+        int cur = 0;
+        for (int len = 3; len <= N3; len *= 3) {
+            const int th = len / 3, o = (len - 3) / 2;
+            __syncthreads();
+            for (int j = lane; j < N3; j += 64) {
+                const int g = j - j % len, jj = j % len, i0 = jj % th;
+                const int64_t bb = ya[cur][g + i0], cc = ya[cur][g + i0 + th], dd = ya[cur][g + i0 + 2 * th];
+                ya[cur ^ 1][j] = trem64(wadd(wadd(bb, wmul((int64_t)T->tw3[o + jj], cc)), wmul((int64_t)T->sq3[o + jj], dd)), P);
+            }
+            cur ^= 1;
+        }
+        __syncthreads();
+        // shares = points[1..=n], clerk-major; CANONICAL: the exact share's canonical residue
+        int64_t* ob = out + vec * (uint64_t)(N3 - 1) * B + b;
+        for (int j = lane + 1; j < N3; j += 64) {
+            const int64_t v = ya[cur][j];
+            ob[(uint64_t)(j - 1) * B] = (canonical && v < 0) ? v + (int64_t)T->M.p : v;
+        }
     }
 }
 
@@ -639,7 +645,7 @@ hipError_t launch_packed_generate(const PackedGenArgs& args, uint32_t k, uint32_
         default: e = hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(packed_gen_fixup_kernel, dim3(256), dim3(256), 0, s, a.secrets, a.dimension, a.draws, a.out,
+    hipLaunchKernelGGL(packed_gen_fixup_kernel, dim3(512), dim3(64), 0, s, a.secrets, a.dimension, a.draws, a.out,
                        k, t, B, a.n_vectors, (int)L, (int)N3, T, log, a.canonical ? 1 : 0);
     return hipGetLastError();
 }
