@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from sda_amd import SdaError, schemes as S
+from sda_amd import engine as E
 from tests.util import assert_same
 
 pytestmark = pytest.mark.gpu
@@ -220,3 +221,25 @@ def test_slot_cap_overflow_falls_back(engine, oracle, monkeypatch, case):
         assert engine.clerk_decode_combine_dev(m, t.data_ptr(), off, res.data_ptr(), D) == D
         torch.cuda.synchronize()
         assert_same(res.cpu().numpy(), exp, f"{case} {path}")
+
+
+def test_encode_dev_capacity(engine, oracle):
+    """The encode places its rows on the device; a dst_cap one byte short of the rows' total is refused
+    (ERR_INVALID_ARGUMENT) with nothing written, and the exact capacity works."""
+    m = 2147482801
+    rng = np.random.default_rng(21)
+    x = rng.integers(-(m - 1), m, size=(5, 3001), dtype=np.int64)
+    total = sum(len(oracle.varint_encode(r)) for r in x)
+    xd = torch.as_tensor(x).cuda()
+    buf = torch.full((total + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    with pytest.raises(SdaError) as ei:
+        engine.varint_encode_dev(xd.data_ptr(), 5, 3001, 3001, buf.data_ptr(), total - 1)
+    assert ei.value.status == E.ERR_INVALID_ARGUMENT
+    torch.cuda.synchronize()
+    assert (buf.cpu().numpy() == 0xA5).all()
+    rb = engine.varint_encode_dev(xd.data_ptr(), 5, 3001, 3001, buf.data_ptr(), total)
+    torch.cuda.synchronize()
+    assert int(rb.sum()) == total
+    host = buf.cpu().numpy().tobytes()
+    assert host[:total] == b"".join(oracle.varint_encode(r) for r in x)
+    assert (buf.cpu().numpy()[total:] == 0xA5).all()
