@@ -443,11 +443,24 @@ static_assert(kRegionBytes / 5 > kScMaxTile && kSlotCap <= (1u << 14) && kScMaxT
 __device__ __forceinline__ uint64_t slot_plan_entry(uint64_t s0, uint64_t c0, uint64_t gap) {
     return s0 | (c0 << 39) | (gap << 50);      // s0: 39 bits, c0: 11 bits, gap: 14 bits
 }
+// The plan and the combine run right behind the decode, before the host has seen the element counts; both
+// exit at once when `flags` is set (bit 0: an element the slots cannot hold -- the job takes the matrix
+// path; bit 1: the blobs decode to different lengths -- "Wrong dimension"), and the combine also when the
+// dimension exceeds the output's capacity.  The host reports those cases after the call's final wait.
+__global__ __launch_bounds__(kThreads) void slot_dims_kernel(const uint64_t* __restrict__ blob_count, uint64_t n_blobs,
+                                                             uint32_t* __restrict__ flags) {
+    bool bad = false;
+    for (uint64_t b = threadIdx.x; b < n_blobs; b += kThreads) bad |= blob_count[b] != blob_count[0];
+    if (bad) atomicOr(flags, 2u);
+}
+
 __global__ __launch_bounds__(kThreads) void slot_plan_kernel(const uint64_t* __restrict__ blob_region,
                                                              const uint64_t* __restrict__ region_base,
                                                              const uint32_t* __restrict__ region_count, uint32_t y0,
                                                              uint64_t n_blobs, uint64_t ntiles, uint32_t tile,
+                                                             const uint32_t* __restrict__ flags,
                                                              uint64_t* __restrict__ plan) {
+    if (*flags) return;
     const uint64_t b = y0 + blockIdx.y;
     const uint64_t r0 = blob_region[b], r1 = blob_region[b + 1];
     const uint64_t r = r0 + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -466,17 +479,21 @@ __global__ __launch_bounds__(kThreads) void slot_plan_kernel(const uint64_t* __r
 // through combiner.rs:16-28's exact recurrence (add_trem).  Blobs go UNROLL at a time: their plan entries
 // are uniform (scalar loads) and give every slot address directly, so all UNROLL slot loads are issued
 // before the dependent chain.  The one lane whose columns straddle the region boundary (c0) also loads
-// them past the gap and merges.  Every blob decoded to `dim` elements (checked on the host before the
-// launch); a lane's load may run past the blob's last element into unused slots (never past the buffer:
-// the tile plan follows the slots).
+// them past the gap and merges.  dim = blob 0's element count, read on the device; the grid covers the
+// host's bound (blob 0's bytes), and runs only when every blob decoded to dim elements (flags clear); a
+// lane's load may run past the blob's last element into unused slots (never past the buffer: the tile
+// plan follows the slots).
 template <int CPL, int UNROLL, bool SMALL_M>
 __global__ __launch_bounds__(kThreads) void slot_combine_kernel(const int32_t* __restrict__ slots,
                                                                 const uint64_t* __restrict__ plan,
-                                                                uint64_t n_blobs, uint64_t dim,
+                                                                uint64_t n_blobs, const uint64_t* __restrict__ dim_p,
+                                                                const uint32_t* __restrict__ flags, uint64_t out_cap,
                                                                 int64_t* __restrict__ out, Mod64 M) {
     typedef typename std::conditional<CPL == 1, int32_t,
             int32_t __attribute__((ext_vector_type(CPL == 1 ? 2 : CPL)))>::type V;
     constexpr uint32_t kTile = CPL * kThreads;
+    const uint64_t dim = *dim_p;
+    if (*flags || dim > out_cap) return;
     const uint64_t e0 = (uint64_t)blockIdx.x * kTile;
     const uint32_t o = CPL * threadIdx.x;
     if (e0 + o >= dim) return;
@@ -1141,12 +1158,19 @@ size_t varint_slot_bytes(const VarintPlan& plan, uint64_t n_blobs, uint64_t dim)
     return (plan.regions * kSlotCap + (kRegionBytes - kSlotCap)) * sizeof(int32_t) + ntiles * n_blobs * 8 + 256;
 }
 
-hipError_t launch_varint_decode_slots(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
-                                      const VarintPlan& plan, void* work, void* slot_buf, uint64_t* counts_host,
-                                      bool* wide_host, hipStream_t s) {
+hipError_t launch_varint_decode_slots_combine(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
+                                              const VarintPlan& plan, void* work, void* slot_buf, int64_t* out,
+                                              uint64_t out_cap, int64_t modulus, uint64_t* counts_host,
+                                              uint32_t* flags_host, hipStream_t s) {
     const size_t R = plan.regions;
     DecodeWork w = carve(work, R, n_blobs);
     int32_t* slots = static_cast<int32_t*>(slot_buf);
+    uint64_t* tplan = reinterpret_cast<uint64_t*>(static_cast<char*>(slot_buf) +
+                                                  (R * kSlotCap + (kRegionBytes - kSlotCap)) * sizeof(int32_t));
+    const uint32_t cpl = slot_cpl(), tile = cpl * kThreads;
+    // the grid's bound: blob 0 decodes to at most one element per byte
+    const uint64_t ntiles = (blob_off_host[1] - blob_off_host[0] + tile - 1) / tile;
+    if (ntiles > 0x7FFFFFFFull || R * kSlotCap >= (1ull << 39)) return hipErrorInvalidValue;
     hipError_t e;
     if ((e = hipMemcpyAsync(w.blob_off, blob_off_host, (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     if ((e = hipMemcpyAsync(w.blob_region, plan.blob_region.data(), (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
@@ -1161,42 +1185,32 @@ hipError_t launch_varint_decode_slots(const uint8_t* bytes, const uint64_t* blob
     hipLaunchKernelGGL(varint_scan_kernel, dim3((unsigned)n_blobs), dim3(kThreads), 0, s, w.region_count,
                        w.blob_region, w.region_base, w.blob_count);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    uint32_t flag = 0;
-    if ((e = hipMemcpyAsync(counts_host, w.blob_count, n_blobs * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(&flag, w.wide, sizeof(flag), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    *wide_host = flag != 0;
-    return hipSuccess;
-}
-
-hipError_t launch_slot_combine(const VarintPlan& plan, void* work, const void* slot_buf, uint64_t n_blobs,
-                               uint64_t dim, int64_t* out, int64_t modulus, hipStream_t s) {
-    if (dim == 0 || n_blobs == 0) return hipSuccess;
-    const size_t R = plan.regions;
-    DecodeWork w = carve(work, R, n_blobs);
-    const int32_t* slots = static_cast<const int32_t*>(slot_buf);
-    uint64_t* tplan = reinterpret_cast<uint64_t*>(const_cast<char*>(static_cast<const char*>(slot_buf)) +
-                                                  (R * kSlotCap + (kRegionBytes - kSlotCap)) * sizeof(int32_t));
-    const uint32_t cpl = slot_cpl(), tile = cpl * kThreads;
-    const uint64_t ntiles = (dim + tile - 1) / tile;
-    if (ntiles > 0x7FFFFFFFull || R * kSlotCap >= (1ull << 39)) return hipErrorInvalidValue;
-    hipError_t e;
-    for (uint64_t y0 = 0; y0 < n_blobs; y0 += 65535) {
-        const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
-        hipLaunchKernelGGL(slot_plan_kernel, dim3((unsigned)((plan.max_regions + kThreads - 1) / kThreads), ny),
-                           dim3(kThreads), 0, s, w.blob_region, w.region_base, w.region_count, (uint32_t)y0, n_blobs,
-                           ntiles, tile, tplan);
+    hipLaunchKernelGGL(slot_dims_kernel, dim3(1), dim3(kThreads), 0, s, (const uint64_t*)w.blob_count, n_blobs, w.wide);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ntiles && modulus > 0) {       // modulus 0: invalid -- no combine (an error if the dimension is > 0)
+        for (uint64_t y0 = 0; y0 < n_blobs; y0 += 65535) {
+            const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
+            hipLaunchKernelGGL(slot_plan_kernel, dim3((unsigned)((plan.max_regions + kThreads - 1) / kThreads), ny),
+                               dim3(kThreads), 0, s, w.blob_region, w.region_base, w.region_count, (uint32_t)y0,
+                               n_blobs, ntiles, tile, (const uint32_t*)w.wide, tplan);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        const Mod64 M = make_mod64(modulus);
+        const bool small_m = modulus <= ((int64_t)1 << 62);
+        const dim3 g((unsigned)ntiles), blk(kThreads);
+#define SLOT_LAUNCH(C, SM)                                                                                 \
+    hipLaunchKernelGGL((slot_combine_kernel<C, 8, SM>), g, blk, 0, s, slots, (const uint64_t*)tplan, n_blobs, \
+                       (const uint64_t*)w.blob_count, (const uint32_t*)w.wide, out_cap, out, M)
+        if (cpl == 4) { if (small_m) SLOT_LAUNCH(4, true); else SLOT_LAUNCH(4, false); }
+        else if (cpl == 2) { if (small_m) SLOT_LAUNCH(2, true); else SLOT_LAUNCH(2, false); }
+        else { if (small_m) SLOT_LAUNCH(1, true); else SLOT_LAUNCH(1, false); }
+#undef SLOT_LAUNCH
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    const Mod64 M = make_mod64(modulus);
-    const bool small_m = modulus <= ((int64_t)1 << 62);
-    const dim3 g((unsigned)ntiles), blk(kThreads);
-#define SLOT_LAUNCH(C, SM) hipLaunchKernelGGL((slot_combine_kernel<C, 8, SM>), g, blk, 0, s, slots, tplan, n_blobs, dim, out, M)
-    if (cpl == 4) { if (small_m) SLOT_LAUNCH(4, true); else SLOT_LAUNCH(4, false); }
-    else if (cpl == 2) { if (small_m) SLOT_LAUNCH(2, true); else SLOT_LAUNCH(2, false); }
-    else { if (small_m) SLOT_LAUNCH(1, true); else SLOT_LAUNCH(1, false); }
-#undef SLOT_LAUNCH
-    return hipGetLastError();
+    // the call's one wait: the counts and the flags, after the whole job
+    if ((e = hipMemcpyAsync(counts_host, w.blob_count, n_blobs * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(flags_host, w.wide, sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    return hipStreamSynchronize(s);
 }
 
 hipError_t launch_varint_decode_combine(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,

@@ -854,10 +854,14 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
         const uint64_t dim_max = blob_off[1] - blob_off[0];
         if (sda_status e = ensure(&h->codec_mat, &h->codec_mat_bytes, sda::varint_slot_bytes(plan, n_blobs, dim_max)))
             return e;
-        bool wide = false;
-        HIP_TRY(sda::launch_varint_decode_slots(bytes, blob_off, n_blobs, plan, h->codec_work, h->codec_mat,
-                                                counts.data(), &wide, st));
-        if (!wide) {
+        // everything is queued before the host sees a count: the combine itself exits when a flag is set
+        // or blob 0's count exceeds out_cap, and the checks below then report it in the reference's order
+        const bool m_ok = m != 0 && m != INT64_MIN;
+        uint32_t flags = 0;
+        HIP_TRY(sda::launch_varint_decode_slots_combine(bytes, blob_off, n_blobs, plan, h->codec_work, h->codec_mat,
+                                                        out, out_cap, m_ok ? (m < 0 ? -m : m) : 0, counts.data(),
+                                                        &flags, st));
+        if (!(flags & 1u)) {
             const uint64_t dim = counts[0];
             for (uint64_t i = 1; i < n_blobs; ++i)
                 if (counts[i] != dim)
@@ -870,8 +874,6 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
             }
             if (out_cap < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
             *out_len = dim;
-            if (dim == 0) return ok();
-            HIP_TRY(sda::launch_slot_combine(plan, h->codec_work, h->codec_mat, n_blobs, dim, out, mm, st));
             return SDA_OK;
         }
     }

@@ -137,16 +137,17 @@ uint64_t varint_fused_tiles(uint64_t dim);
 hipError_t launch_varint_decode_combine(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
                                         uint64_t* tile_plan, uint64_t dim, int64_t* out, int64_t modulus,
                                         bool multi, hipStream_t s);
-// The clerk's decode -> combine over region slots (no count pass): the payload is decoded once into int32
-// slots per 16 KiB region (slot buffer: varint_slot_bytes), region counts scanned; counts_host[n_blobs]
-// and *wide_host (some element longer than 5 bytes or not a field share: use the matrix path) are
-// synchronous.  Then launch_slot_combine runs combiner.rs:16-28 over the slots (every blob has dim values).
+// The clerk's decode -> combine over region slots (no count pass), in one pass of launches: the payload is
+// decoded once into int32 slots per 16 KiB region (slot buffer: varint_slot_bytes), region counts are
+// scanned, and combiner.rs:16-28 runs over the slots into out -- unless *flags_host comes back nonzero
+// (bit 0: an element longer than 5 bytes or not a field share: use the matrix path; bit 1: the blobs
+// decode to different lengths), or blob 0's count exceeds out_cap, or modulus (|m|) is 0: then out is
+// untouched.  counts_host[n_blobs] and *flags_host are read at the end of the call (its only wait).
 size_t varint_slot_bytes(const VarintPlan& plan, uint64_t n_blobs, uint64_t dim);
-hipError_t launch_varint_decode_slots(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
-                                      const VarintPlan& plan, void* work, void* slot_buf, uint64_t* counts_host,
-                                      bool* wide_host, hipStream_t s);
-hipError_t launch_slot_combine(const VarintPlan& plan, void* work, const void* slot_buf, uint64_t n_blobs,
-                               uint64_t dim, int64_t* out, int64_t modulus, hipStream_t s);
+hipError_t launch_varint_decode_slots_combine(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
+                                              const VarintPlan& plan, void* work, void* slot_buf, int64_t* out,
+                                              uint64_t out_cap, int64_t modulus, uint64_t* counts_host,
+                                              uint32_t* flags_host, hipStream_t s);
 size_t varint_encode_work_bytes(uint64_t rows, uint64_t len);
 // encode rows [rows][stride] (first len elements) back to back into dst; row_bytes_host gets each
 // row's byte count (synchronous).  hipErrorInvalidValue if dst_cap is too small.

@@ -243,3 +243,34 @@ def test_encode_dev_capacity(engine, oracle):
     host = buf.cpu().numpy().tobytes()
     assert host[:total] == b"".join(oracle.varint_encode(r) for r in x)
     assert (buf.cpu().numpy()[total:] == 0xA5).all()
+
+
+@pytest.mark.parametrize("path", ["slots", "matrix"])
+def test_decode_combine_errors_leave_output(engine, oracle, monkeypatch, path):
+    """The slot path queues its combine before the host has seen the element counts; the combine exits on
+    the device when the blobs decode to different lengths, when the dimension exceeds out_cap, or when the
+    modulus is invalid -- the call then returns the reference's error and `out` is untouched.  (m = 0 with
+    only empty blobs is no error: combiner.rs computes no %.)"""
+    monkeypatch.setenv("SDA_CODEC_PATH", path)
+    m = 2147482801
+    rng = np.random.default_rng(31)
+    rows = [rng.integers(-(m - 1), m, size=5000, dtype=np.int64) for _ in range(4)]
+    good = [oracle.varint_encode(r) for r in rows]
+    out = torch.full((5000,), 7, dtype=torch.int64, device="cuda")
+
+    def run(blobs, modulus, cap):
+        t, off = _pack(blobs)
+        return engine.clerk_decode_combine_dev(modulus, t.data_ptr(), off, out.data_ptr(), cap)
+
+    bad = good[:2] + [oracle.varint_encode(rows[2][:4999])] + good[3:]
+    for blobs, modulus, cap, status in ((bad, m, 5000, E.ERR_WRONG_DIMENSION), (good, m, 4999, E.ERR_INVALID_ARGUMENT),
+                                        (good, 0, 5000, E.ERR_PRECONDITION)):
+        with pytest.raises(SdaError) as ei:
+            run(blobs, modulus, cap)
+        assert ei.value.status == status
+        torch.cuda.synchronize()
+        assert (out.cpu().numpy() == 7).all()
+    assert run([b"", b""], 0, 5000) == 0
+    assert run(good, m, 5000) == 5000
+    torch.cuda.synchronize()
+    assert_same(out.cpu().numpy(), oracle.combine(m, np.stack(rows)))
