@@ -14,4 +14,4 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $T/trace -o run -- \
     python3 bench.py --only codec --steps 5 --warmup 1 > $T/trace.log 2>&1 || { tail -5 $T/trace.log; exit 1; }
 python3 scripts/stats_by_grid.py $T/trace/run_kernel_trace.csv > $T/stats_by_grid.csv
-grep -E "slot|decode_kernel<int, true>|scan" $T/stats_by_grid.csv | cut -c1-160
+grep -E "slot|decode_kernel|scan|count|cap_kernel|sequential" $T/stats_by_grid.csv | cut -c1-160

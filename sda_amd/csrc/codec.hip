@@ -315,9 +315,11 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
                                                                  const uint32_t* __restrict__ blob_irregular,
                                                                  OutT* __restrict__ out, uint64_t out_stride,
                                                                  uint32_t* __restrict__ wide,
-                                                                 uint32_t* __restrict__ region_count = nullptr) {
+                                                                 uint32_t* __restrict__ region_count = nullptr,
+                                                                 const uint32_t* __restrict__ skip = nullptr) {
     uint32_t b;
     uint64_t r, word;
+    if (skip && *skip) return;                                // a blob exceeds the output row: write nothing
     if (!region_of(blob_region, blob_off, y0, &b, &r, &word)) return;
     if (!SPARSE && (blob_irregular[b] & 1u)) return;
     // LDS holds one sub-region at a time (the region's other words wait in registers): 12.9 KB per
@@ -447,6 +449,14 @@ __device__ __forceinline__ uint64_t slot_plan_entry(uint64_t s0, uint64_t c0, ui
 // exit at once when `flags` is set (bit 0: an element the slots cannot hold -- the job takes the matrix
 // path; bit 1: the blobs decode to different lengths -- "Wrong dimension"), and the combine also when the
 // dimension exceeds the output's capacity.  The host reports those cases after the call's final wait.
+// sda_varint_decode_dev's capacity check on the device: *flag = some blob decodes to more than cap values.
+__global__ __launch_bounds__(kThreads) void varint_cap_kernel(const uint64_t* __restrict__ blob_count, uint64_t n_blobs,
+                                                              uint64_t cap, uint32_t* __restrict__ flag) {
+    bool over = false;
+    for (uint64_t b = threadIdx.x; b < n_blobs; b += kThreads) over |= blob_count[b] > cap;
+    if (over) atomicOr(flag, 1u);
+}
+
 __global__ __launch_bounds__(kThreads) void slot_dims_kernel(const uint64_t* __restrict__ blob_count, uint64_t n_blobs,
                                                              uint32_t* __restrict__ flags) {
     bool bad = false;
@@ -778,9 +788,9 @@ void varint_decode_combine_kernel(const uint8_t* __restrict__ bytes, const uint6
 __global__ void varint_sequential_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ blob_off,
                                          uint32_t n_blobs, const uint32_t* __restrict__ blob_irregular,
                                          uint64_t* __restrict__ blob_count, int64_t* __restrict__ out,
-                                         uint64_t out_stride, uint64_t cap) {
+                                         uint64_t out_stride, uint64_t cap, const uint32_t* __restrict__ skip = nullptr) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= n_blobs || !(blob_irregular[b] & 1u)) return;
+    if (b >= n_blobs || !(blob_irregular[b] & 1u) || (out && skip && *skip)) return;
     uint64_t r = blob_off[b];
     const uint64_t e = blob_off[b + 1];
     uint64_t c = 0;
@@ -1123,6 +1133,51 @@ hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const Va
                            w.blob_off, (uint32_t)n_blobs, w.irregular, w.blob_count, out, out_stride, len);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    return hipSuccess;
+}
+
+hipError_t launch_varint_decode_one_wait(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
+                                        const VarintPlan& plan, void* work, int64_t* out, uint64_t out_stride,
+                                        uint64_t* counts_host, bool* too_long, hipStream_t s) {
+    const size_t R = plan.regions;
+    DecodeWork w = carve(work, R, n_blobs);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(w.blob_off, blob_off_host, (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(w.blob_region, plan.blob_region.data(), (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.irregular, 0, n_blobs * 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.wide, 0, sizeof(uint32_t), s)) != hipSuccess) return e;      // the capacity flag
+    for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
+        const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
+        hipLaunchKernelGGL(varint_count_kernel, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s, bytes,
+                           w.blob_region, w.blob_off, (uint32_t)y0, w.region_count, w.irregular, (uint16_t*)nullptr);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(varint_scan_kernel, dim3((unsigned)n_blobs), dim3(kThreads), 0, s, w.region_count,
+                       w.blob_region, w.region_base, w.blob_count);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const unsigned seq_grid = (unsigned)((n_blobs + 63) / 64);
+    hipLaunchKernelGGL(varint_sequential_kernel, dim3(seq_grid), dim3(64), 0, s, bytes, w.blob_off, (uint32_t)n_blobs,
+                       w.irregular, w.blob_count, (int64_t*)nullptr, 0, 0, (const uint32_t*)nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(varint_cap_kernel, dim3(1), dim3(kThreads), 0, s, (const uint64_t*)w.blob_count, n_blobs,
+                       out_stride, w.wide);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
+        const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
+        hipLaunchKernelGGL(varint_decode_kernel<int64_t>, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s,
+                           bytes, w.blob_region, w.blob_off, (uint32_t)y0, w.region_base, w.irregular, out, out_stride,
+                           (uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)w.wide);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(varint_sequential_kernel, dim3(seq_grid), dim3(64), 0, s, bytes, w.blob_off, (uint32_t)n_blobs,
+                       w.irregular, w.blob_count, out, out_stride, out_stride, (const uint32_t*)w.wide);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the call's one wait: the counts and the capacity flag, after the whole job
+    uint32_t flag = 0;
+    if ((e = hipMemcpyAsync(counts_host, w.blob_count, n_blobs * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(&flag, w.wide, sizeof(flag), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    *too_long = flag != 0;
     return hipSuccess;
 }
 

@@ -1015,14 +1015,24 @@ sda_status sda_varint_decode_dev(sda_engine* h, const uint8_t* bytes, const uint
     if (!h || !blob_off || !counts || (n_blobs && (!bytes || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = pick(h, stream);
+    if (n_blobs == 0) return ok();
+    if (((uintptr_t)bytes & 15) != 0) return fail(SDA_ERR_INVALID_ARGUMENT, "byte buffer must be 16-byte aligned");
+    for (uint64_t b = 0; b < n_blobs; ++b)
+        if (blob_off[b + 1] < blob_off[b]) return fail(SDA_ERR_INVALID_ARGUMENT, "blob offsets must be non-decreasing");
     sda::VarintPlan plan;
-    bool irregular = false;
-    if (sda_status e = codec_count(h, bytes, blob_off, n_blobs, &plan, counts, &irregular, st)) return e;
-    for (uint64_t i = 0; i < n_blobs; ++i)
-        if (counts[i] > out_stride)
-            return fail(SDA_ERR_INVALID_ARGUMENT, "blob %llu decodes to %llu values > out_stride",
-                        (unsigned long long)i, (unsigned long long)counts[i]);
-    HIP_TRY(sda::launch_varint_decode(bytes, n_blobs, plan, h->codec_work, out, out_stride, out_stride, irregular, st));
+    sda::varint_plan(blob_off, n_blobs, &plan);
+    if (sda_status e = ensure(&h->codec_work, &h->codec_work_bytes, sda::varint_decode_work_bytes(plan.regions, n_blobs)))
+        return e;
+    // count, check the capacity and decode without a host wait in between: a blob longer than out_stride
+    // stops every write on the device and is reported here (nothing written)
+    bool too_long = false;
+    HIP_TRY(sda::launch_varint_decode_one_wait(bytes, blob_off, n_blobs, plan, h->codec_work, out, out_stride, counts,
+                                               &too_long, st));
+    if (too_long)
+        for (uint64_t i = 0; i < n_blobs; ++i)
+            if (counts[i] > out_stride)
+                return fail(SDA_ERR_INVALID_ARGUMENT, "blob %llu decodes to %llu values > out_stride",
+                            (unsigned long long)i, (unsigned long long)counts[i]);
     return ok();
 }
 

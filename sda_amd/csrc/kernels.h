@@ -127,6 +127,12 @@ hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const Va
                                 hipStream_t s);
 // the same decode into int32 (regular blobs only: the caller checked irregular_any == false); *wide_host
 // (synchronous) tells whether some value did not fit, in which case out holds garbage
+// sda_varint_decode_dev in one pass of launches: count, scan, a device capacity check (some blob
+// decodes to more than out_stride values: nothing is written, *too_long), decode; counts_host[n_blobs]
+// and the flag are read at the end of the call (its only wait).
+hipError_t launch_varint_decode_one_wait(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
+                                        const VarintPlan& plan, void* work, int64_t* out, uint64_t out_stride,
+                                        uint64_t* counts_host, bool* too_long, hipStream_t s);
 hipError_t launch_varint_decode_narrow(const uint8_t* bytes, uint64_t n_blobs, const VarintPlan& plan, void* work,
                                        int32_t* out, uint64_t out_stride, bool* wide_host, hipStream_t s);
 // The clerk's fused decode -> combine (after launch_varint_count with sub_counts on the same work; regular

@@ -274,3 +274,30 @@ def test_decode_combine_errors_leave_output(engine, oracle, monkeypatch, path):
     assert run(good, m, 5000) == 5000
     torch.cuda.synchronize()
     assert_same(out.cpu().numpy(), oracle.combine(m, np.stack(rows)))
+
+
+@pytest.mark.parametrize("irregular", [False, True])
+def test_decode_dev_capacity_leaves_output(engine, oracle, irregular):
+    """sda_varint_decode_dev counts, checks out_stride and decodes without a host wait in between: a blob
+    with more values than out_stride (a regular one, or a malformed one the sequential decoder takes) stops
+    every write on the device -- the call fails with nothing written; out_stride = the longest blob works."""
+    rng = np.random.default_rng(41)
+    rows = [rng.integers(-(2**40), 2**40, size=n, dtype=np.int64) for n in (3000, 3100, 2900)]
+    blobs = [oracle.varint_encode(r) for r in rows]
+    if irregular:                                   # 12 continuation bytes: u64::decode_var's shift > 70 stop
+        blobs[1] = bytes([0xFF] * 12 + [0x01]) + blobs[1]
+    exp = [oracle.varint_decode(b) for b in blobs]
+    longest = max(e.size for e in exp)
+    t, off = _pack(blobs)
+    out = torch.full((3, longest), 7, dtype=torch.int64, device="cuda")
+    with pytest.raises(SdaError) as ei:
+        engine.varint_decode_dev(t.data_ptr(), off, out.data_ptr(), longest - 1)
+    assert ei.value.status == E.ERR_INVALID_ARGUMENT
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy() == 7).all()
+    counts = engine.varint_decode_dev(t.data_ptr(), off, out.data_ptr(), longest)
+    torch.cuda.synchronize()
+    assert counts.tolist() == [e.size for e in exp]
+    got = out.cpu().numpy()
+    for i, e in enumerate(exp):
+        assert_same(got[i, :e.size], e)
