@@ -21,7 +21,9 @@ ranks' results:
 * an input outside [-(2^63 - m), 2^63 - m]: the reference's running sum may wrap there, which no
   split reproduces -- ValueError (use one rank, or the column split).
 
-At world size 1 no exchange runs and the exact single-pass result is returned as is.  The column split
+At world size 1 no exchange runs and the exact single-pass result is returned as is
+(`EXCHANGE_AT_WORLD_1` = True runs the full exchange path instead, over a one-rank group: how a one-GPU
+box drives RCCL through the very calls of the 8-GPU run, tests/test_gpu_multirank.py).  The column split
 (combine_columns_sharded: each rank owns a slice of D and walks all N rows) stays for callers that
 hold whole columns.
 
@@ -39,6 +41,11 @@ from __future__ import annotations
 from typing import Iterable, Tuple
 
 I64_MAX = (1 << 63) - 1
+EXCHANGE_AT_WORLD_1 = False     # run the collectives even in a one-rank group (module doc)
+
+
+def _exchange(world: int) -> bool:
+    return world > 1 or EXCHANGE_AT_WORLD_1
 
 
 def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -86,7 +93,7 @@ def reduce_canonical(partial, modulus: int, finalize, out, group=None):
     import torch.distributed as dist
 
     world = _world(group)
-    if world == 1:
+    if not _exchange(world):
         out.copy_(partial)
         return
     if not reduce_headroom_ok(world, modulus):
@@ -115,7 +122,7 @@ def _combine_split(engine, modulus: int, tiles, dim: int, row_stride: int, parti
     stats = stats if stats is not None else SplitStats()
     stats.signed, stats.passes = False, 1
     with _on(partial, st):
-        if world == 1:               # one sequential pass: the exact result, signed values included
+        if not _exchange(world):     # one sequential pass: the exact result, signed values included
             if len(tiles) == 1:
                 engine.combine_dev(modulus, tiles[0][0], tiles[0][1], dim, row_stride, partial.data_ptr(), st)
             else:
@@ -216,7 +223,7 @@ def combine_columns_sharded(engine, modulus: int, shares, out, group=None, strea
         if cnt:
             engine.combine_dev(modulus, shares[:, lo:].data_ptr(), n, cnt, shares.stride(0), mine.data_ptr(), st)
         parts = [torch.empty_like(mine) for _ in range(world)]
-        if world > 1:
+        if _exchange(world):
             dist.all_gather(parts, mine, group=group)
         else:
             parts = [mine]

@@ -1,5 +1,6 @@
 """One rank of tests/test_gpu_multirank.py: the product's multi-GPU helpers (sda_amd.distributed) on the
-HIP engine, two ranks sharing one MI355X (cuda:0) over gloo.
+HIP engine, two or four ranks sharing one MI355X (cuda:0) over gloo -- or one rank over RCCL
+(SDA_MR_BACKEND=nccl) with the exchange path forced at world size 1.
 
 Not a test module: test_gpu_multirank starts two of these as plain child processes (RANK 0 and 1),
 so the collective path of bench.py --gpus N runs with the real device kernels and real device tensors;
@@ -34,9 +35,14 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
     torch.cuda.init()
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    backend = os.environ.get("SDA_MR_BACKEND", "gloo")
+    if backend == "nccl":          # RCCL: one rank per device, so world 1 here
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     from sda_amd import Engine, synth
     from sda_amd import distributed as Dd
+    Dd.EXCHANGE_AT_WORLD_1 = world == 1     # world 1: the same collectives over a one-rank group
 
     eng = Engine(0)
     dev = torch.device("cuda", 0)

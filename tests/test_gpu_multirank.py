@@ -4,7 +4,10 @@ Child processes (tests/multirank_worker.py, one per RANK) share cuda:0 and a glo
 each runs the engine's device kernels on its own participations / seeds / column slice, and the
 product functions do the exchange (int64 all-reduce + device finalize, or all-gather) on device
 tensors -- the code path of `bench.py --gpus N`, with gloo standing in for RCCL (RCCL refuses two
-ranks on one device; the 8-GPU node runs the same calls over RCCL).  The results must equal the
+ranks on one device; the 8-GPU node runs the same calls over RCCL).  The third case runs ONE rank over
+RCCL with the exchange forced at world size 1 (distributed.EXCHANGE_AT_WORLD_1): every RCCL call of the
+8-GPU path -- int64 SUM all-reduce, the flag readback, all-gather into row views, int32 MAX all-reduce --
+on real device tensors, against the same oracle results.  The results must equal the
 reference's single sequential pass (combiner.rs:16-28, chacha.rs:57-76), recomputed by the oracle.
 """
 import os
@@ -32,12 +35,13 @@ def _free_port():
     return port
 
 
-@pytest.fixture(scope="module", params=[2, 4], ids=["world2", "world4"])
+@pytest.fixture(scope="module", params=[(2, "gloo"), (4, "gloo"), (1, "nccl")],
+                ids=["world2", "world4", "rccl_world1"])
 def results(request, tmp_path_factory):
-    world = request.param
+    world, backend = request.param
     out = str(tmp_path_factory.mktemp("mr") / "res.npz")
     env = dict(os.environ, WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
-               SDA_MR_OUT=out, PYTHONUNBUFFERED="1")
+               SDA_MR_OUT=out, SDA_MR_BACKEND=backend, PYTHONUNBUFFERED="1")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "multirank_worker.py")],
                               env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
