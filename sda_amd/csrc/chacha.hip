@@ -73,14 +73,10 @@ struct RejectLog {
 // write-back is coalesced (lane t writes element t + 256 j): plain stores when the grid has a
 // single seed chunk (DIRECT: acc is the output), atomics into acc otherwise.
 constexpr int kChachaPad = 9;                  // LDS row stride (u64) of a lane's 8 results
-// ADD (DIRECT, one stream: the participant's mask, chacha.rs:36-45): acc[e] = (secrets[e] + draw) % m
-// instead of the draw -- the mask itself is never stored.
-template <bool LAZY, bool DIRECT, bool ADD = false>
+template <bool LAZY, bool DIRECT>
 __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __restrict__ seeds, uint32_t w, uint64_t n_seeds,
                            uint64_t seeds_per_chunk, uint64_t D, unsigned long long* __restrict__ acc, Mod64 M,
-                           uint64_t zone, uint64_t r64, RejectLog log,
-                           const int64_t* __restrict__ secrets = nullptr, bool small_m = false) {
-    static_assert(DIRECT || !ADD, "ADD needs the single-chunk grid");
+                           uint64_t zone, uint64_t r64, RejectLog log) {
     __shared__ unsigned long long st[256 * kChachaPad];
     const uint32_t tid = threadIdx.x;
     const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + tid;
@@ -138,10 +134,53 @@ __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __r
         const uint64_t e = e0 + idx;
         if (e < D) {
             const unsigned long long r = st[(idx >> 3) * kChachaPad + (idx & 7)];
-            if constexpr (ADD) acc[e] = (unsigned long long)add_trem((int64_t)r, secrets[e], M, small_m);
-            else if constexpr (DIRECT) acc[e] = r;
+            if constexpr (DIRECT) acc[e] = r;
             else atomicAdd(&acc[e], r);
         }
+    }
+}
+
+// One stream, the participant's mask (chacha.rs:36-45): out[e] = (secrets[e] + draw_e) % m; the mask itself
+// is never stored.  A lane owns the 8 draws of ChaCha block `blk` (as in chacha_combine_kernel, whose
+// reduction of a single draw is umod64(v) on both of its paths).  The lane's 8 secrets -- elements
+// e0 + 256 j + tid, the coalesced write-back order -- are loaded before the block is computed, so their
+// latency hides under the ChaCha rounds instead of following them.
+__global__ __launch_bounds__(256) void chacha_mask_add_kernel(const uint32_t* __restrict__ seeds, uint32_t w, uint64_t D,
+                                                              unsigned long long* __restrict__ out, Mod64 M,
+                                                              uint64_t zone, RejectLog log,
+                                                              const int64_t* __restrict__ secrets, bool small_m) {
+    __shared__ unsigned long long st[256 * kChachaPad];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + tid;
+    const uint64_t e0 = (uint64_t)blockIdx.x * 2048;
+    int64_t sec[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint64_t e = e0 + j * 256 + tid;
+        sec[j] = e < D ? __builtin_nontemporal_load(secrets + e) : 0;
+    }
+    const uint32_t nw = w < 8 ? w : 8;
+    uint32_t key[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) key[q] = (uint32_t)q < nw ? seeds[q] : 0u;
+    uint32_t o[16];
+    chacha_block(key, blk, o);
+    const uint32_t nvalid = blk * 8 >= D ? 0u : (D - blk * 8 < 8 ? (uint32_t)(D - blk * 8) : 8u);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint64_t v = ((uint64_t)o[2 * q] << 32) | o[2 * q + 1];      // high word first
+        if ((uint32_t)q < nvalid && v >= zone) {                         // rejected: log it
+            const unsigned long long slot = atomicAdd(log.count, 1ull);
+            if (slot < log.cap) { log.seed_of[slot] = 0u; log.pair_of[slot] = blk * 8 + q; }
+        }
+        st[tid * kChachaPad + q] = umod64(v, M);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t idx = j * 256 + tid;
+        const uint64_t e = e0 + idx;
+        if (e < D) out[e] = (unsigned long long)add_trem((int64_t)st[(idx >> 3) * kChachaPad + (idx & 7)], sec[j], M, small_m);
     }
 }
 
@@ -407,7 +446,7 @@ hipError_t launch_chacha_stream(int64_t modulus, uint64_t D, const uint32_t* see
 // stream has drained, chacha_fast_resolve applies the fix-ups for that count (rare: each draw is
 // rejected with probability < 2^-28 on this path) or reports a log overflow (the caller then runs the
 // stream path).
-// secrets != nullptr (one seed): out = (secrets + draw) % m, the masked secrets (ADD kernel).
+// secrets != nullptr (one seed): out = (secrets + draw) % m, the masked secrets (chacha_mask_add_kernel).
 static hipError_t chacha_fast_enqueue(int64_t modulus, uint64_t D, const uint32_t* seeds_dev, uint32_t w,
                                       uint64_t n_seeds, int64_t* out, void* work, hipStream_t s,
                                       unsigned long long* count_host, const int64_t* secrets = nullptr) {
@@ -469,12 +508,9 @@ static hipError_t chacha_fast_enqueue(int64_t modulus, uint64_t D, const uint32_
     hipLaunchKernelGGL((chacha_combine_kernel<L, DI>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per, D, \
                        dst, M, zone, r64, log)
     const bool small_m = mm <= (1ull << 62);
-    if (secrets && lazy)
-        hipLaunchKernelGGL((chacha_combine_kernel<true, true, true>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds,
-                           per, D, dst, M, zone, r64, log, secrets, small_m);
-    else if (secrets)
-        hipLaunchKernelGGL((chacha_combine_kernel<false, true, true>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds,
-                           per, D, dst, M, zone, r64, log, secrets, small_m);
+    if (secrets)
+        hipLaunchKernelGGL(chacha_mask_add_kernel, dim3((unsigned)gx), dim3(256), 0, s, seeds_dev, w, D, dst, M, zone,
+                           log, secrets, small_m);
     else if (lazy && direct) SDA_CHACHA_LAUNCH(true, true);
     else if (lazy) SDA_CHACHA_LAUNCH(true, false);
     else if (direct) SDA_CHACHA_LAUNCH(false, true);
