@@ -40,6 +40,40 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return __builtin_a
 
 struct Key8 { uint32_t k[8]; };
 
+// Round 1's column quarter-rounds on columns 1-3 read only the key, the constants and the counter's high
+// word -- per stream (and per workgroup) uniform -- so a kernel that walks many blocks of one stream per
+// iteration computes them once, as scalar code, and hands them to chacha_block_pre.
+struct ChachaPre {
+    uint32_t x1, x5, x9, x13, x2, x6, x10, x14, x3, x7, x11, x15;
+};
+
+__device__ __forceinline__ ChachaPre chacha_pre(const uint32_t* key, uint32_t ctr_hi) {
+    ChachaPre P{C1, key[1], key[5], ctr_hi, C2, key[2], key[6], 0u, C3, key[3], key[7], 0u};
+    SDA_QR(P.x1, P.x5, P.x9, P.x13);
+    SDA_QR(P.x2, P.x6, P.x10, P.x14);
+    SDA_QR(P.x3, P.x7, P.x11, P.x15);
+    return P;
+}
+
+// chacha_block with round 1's columns 1-3 taken from P (= chacha_pre(key, counter >> 32))
+__device__ __forceinline__ void chacha_block_pre(const ChachaPre& P, const uint32_t* key, uint64_t counter,
+                                                 uint32_t (&o)[16]) {
+    uint32_t x0 = C0, x4 = key[0], x8 = key[4], x12 = (uint32_t)counter;
+    uint32_t x1 = P.x1, x5 = P.x5, x9 = P.x9, x13 = P.x13, x2 = P.x2, x6 = P.x6, x10 = P.x10, x14 = P.x14;
+    uint32_t x3 = P.x3, x7 = P.x7, x11 = P.x11, x15 = P.x15;
+    SDA_QR(x0, x4, x8, x12);
+    SDA_QR(x0, x5, x10, x15); SDA_QR(x1, x6, x11, x12); SDA_QR(x2, x7, x8, x13); SDA_QR(x3, x4, x9, x14);
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        SDA_QR(x0, x4, x8, x12); SDA_QR(x1, x5, x9, x13); SDA_QR(x2, x6, x10, x14); SDA_QR(x3, x7, x11, x15);
+        SDA_QR(x0, x5, x10, x15); SDA_QR(x1, x6, x11, x12); SDA_QR(x2, x7, x8, x13); SDA_QR(x3, x4, x9, x14);
+    }
+    o[0] = x0 + C0; o[1] = x1 + C1; o[2] = x2 + C2; o[3] = x3 + C3;
+    o[4] = x4 + key[0]; o[5] = x5 + key[1]; o[6] = x6 + key[2]; o[7] = x7 + key[3];
+    o[8] = x8 + key[4]; o[9] = x9 + key[5]; o[10] = x10 + key[6]; o[11] = x11 + key[7];
+    o[12] = x12 + (uint32_t)counter; o[13] = x13 + (uint32_t)(counter >> 32); o[14] = x14; o[15] = x15;
+}
+
 // one ChaCha20 block: core(state) = rounds(state) + state
 __device__ __forceinline__ void chacha_block(const uint32_t* key, uint64_t counter, uint32_t (&o)[16]) {
     uint32_t x0 = C0, x1 = C1, x2 = C2, x3 = C3;
@@ -73,20 +107,27 @@ struct RejectLog {
 // write-back is coalesced (lane t writes element t + 256 j): plain stores when the grid has a
 // single seed chunk (DIRECT: acc is the output), atomics into acc otherwise.
 constexpr int kChachaPad = 9;                  // LDS row stride (u64) of a lane's 8 results
-template <bool LAZY, bool DIRECT>
+// PRE: round 1's uniform columns of every seed come precomputed from `pre` (chacha_pre_kernel, counter
+// high word 0: the grid then holds < 2^32 blocks); otherwise the kernel computes them per seed.
+template <bool LAZY, bool DIRECT, bool PRE = false>
 __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __restrict__ seeds, uint32_t w, uint64_t n_seeds,
                            uint64_t seeds_per_chunk, uint64_t D, unsigned long long* __restrict__ acc, Mod64 M,
-                           uint64_t zone, uint64_t r64, RejectLog log) {
+                           uint64_t zone, uint64_t r64, RejectLog log, const ChachaPre* __restrict__ pre = nullptr) {
     __shared__ unsigned long long st[256 * kChachaPad];
     const uint32_t tid = threadIdx.x;
     const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + tid;
     const uint64_t n_blk = (D + 7) / 8;
     const bool live = blk < n_blk;
     const uint64_t s0 = (uint64_t)blockIdx.y * seeds_per_chunk;
-    const uint64_t s1 = live ? (s0 + seeds_per_chunk < n_seeds ? s0 + seeds_per_chunk : n_seeds) : s0;
+    // the seed loop is uniform (lanes past D run it on draws they never keep), so each seed's key and
+    // round-1 columns 1-3 are scalar work; a 256-block group never straddles 2^32, so the counter's high
+    // word is uniform too
+    const uint64_t s1 = s0 + seeds_per_chunk < n_seeds ? s0 + seeds_per_chunk : n_seeds;
+    const uint32_t ctr_hi = (uint32_t)(((uint64_t)blockIdx.x * blockDim.x) >> 32);
     const uint32_t nw = w < 8 ? w : 8;
     const uint64_t m = M.m;
     const uint32_t nvalid = !live ? 0u : (D - blk * 8 < 8 ? (uint32_t)(D - blk * 8) : 8u);   // pairs inside D
+    const uint32_t zone_hi = (uint32_t)(zone >> 32);     // v >= zone needs hi(v) >= zone_hi
     uint64_t a[8];
     uint32_t hi[8];
 #pragma unroll
@@ -96,23 +137,30 @@ __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __r
 #pragma unroll
         for (int q = 0; q < 8; ++q) key[q] = (uint32_t)q < nw ? seeds[s * w + q] : 0u;   // uniform: scalar loads
         uint32_t o[16];
-        chacha_block(key, blk, o);
+        chacha_block_pre(PRE ? pre[s] : chacha_pre(key, ctr_hi), key, blk, o);
+        // rejections (< 2^-28 per draw): one max over the 8 high words screens the block
+        const uint32_t hmax = max(max(max(o[0], o[2]), max(o[4], o[6])), max(max(o[8], o[10]), max(o[12], o[14])));
+        if (hmax >= zone_hi) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const uint64_t v = ((uint64_t)o[2 * q] << 32) | o[2 * q + 1];    // high word first
-            if ((uint32_t)q < nvalid) {
-                if (v >= zone) {                                            // rejected: log it
+            for (int q = 0; q < 8; ++q) {
+                const uint64_t v = ((uint64_t)o[2 * q] << 32) | o[2 * q + 1];
+                if ((uint32_t)q < nvalid && v >= zone) {                    // rejected: log it
                     const unsigned long long slot = atomicAdd(log.count, 1ull);
                     if (slot < log.cap) { log.seed_of[slot] = (uint32_t)s; log.pair_of[slot] = blk * 8 + q; }
                 }
-                if constexpr (LAZY) {
-                    const uint64_t x = a[q] + v;
-                    hi[q] += x < v ? 1u : 0u;
-                    a[q] = x;
-                } else {
-                    uint64_t x = a[q] + umod64(v, M);
-                    a[q] = x >= m ? x - m : x;
-                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t v = ((uint64_t)o[2 * q] << 32) | o[2 * q + 1];    // high word first
+            // pairs past D are summed too and never stored (only the last block of the grid has any)
+            if constexpr (LAZY) {
+                const uint64_t x = a[q] + v;
+                hi[q] += x < v ? 1u : 0u;
+                a[q] = x;
+            } else {
+                uint64_t x = a[q] + umod64(v, M);
+                a[q] = x >= m ? x - m : x;
             }
         }
     }
@@ -138,6 +186,18 @@ __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __r
             else atomicAdd(&acc[e], r);
         }
     }
+}
+
+// chacha_pre of every seed (counter high word 0), one lane per seed, for chacha_combine_kernel<PRE>
+__global__ __launch_bounds__(256) void chacha_pre_kernel(const uint32_t* __restrict__ seeds, uint32_t w, uint64_t n_seeds,
+                                                         ChachaPre* __restrict__ pre) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_seeds) return;
+    const uint32_t nw = w < 8 ? w : 8;
+    uint32_t key[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) key[q] = (uint32_t)q < nw ? seeds[s * w + q] : 0u;
+    pre[s] = chacha_pre(key, 0u);
 }
 
 // One stream, the participant's mask (chacha.rs:36-45): out[e] = (secrets[e] + draw_e) % m; the mask itself
@@ -352,10 +412,13 @@ __global__ __launch_bounds__(256) void chacha_stream_scatter_kernel(const uint32
 }  // namespace
 
 // ---- fast path: work layout [acc: D u64][count u64][seed_of: cap u32][pair_of: cap u64][rej upload: cap u64]
+//      [pre: n_seeds ChachaPre, 64-byte aligned]
 static constexpr uint64_t kRejectCap = 1 << 16;
 
-size_t chacha_work_bytes(uint64_t dimension) {
-    return dimension * 8 + 16 + kRejectCap * (4 + 8 + 8) + 64;
+static uint64_t chacha_pre_off(uint64_t D) { return (D * 8 + 16 + kRejectCap * (4 + 8 + 8) + 63) & ~(uint64_t)63; }
+
+size_t chacha_work_bytes(uint64_t dimension, uint64_t n_seeds) {
+    return chacha_pre_off(dimension) + n_seeds * sizeof(ChachaPre) + 64;
 }
 
 bool chacha_needs_stream_path(int64_t modulus) {
@@ -474,11 +537,11 @@ static hipError_t chacha_fast_enqueue(int64_t modulus, uint64_t D, const uint32_
     if (cap_wgs == 0) {
         int cus = 0, per_cu = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chacha_combine_kernel<true, false>, 256, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chacha_combine_kernel<true, false, true>, 256, 0);
         // the API can be one block per CU high at 81-96 SGPRs (MI355X_MICROARCH.md): also bound it by
         // the VGPR allocation (8-register granule, 512 per SIMD lane, 4 waves per block of 256)
         hipFuncAttributes fa{};
-        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(chacha_combine_kernel<true, false>)) == hipSuccess &&
+        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(chacha_combine_kernel<true, false, true>)) == hipSuccess &&
             fa.numRegs > 0) {
             const int by_vgpr = 512 / (((fa.numRegs + 7) / 8) * 8);
             if (by_vgpr < per_cu) per_cu = by_vgpr;
@@ -504,9 +567,23 @@ static hipError_t chacha_fast_enqueue(int64_t modulus, uint64_t D, const uint32_
     RejectLog log{count, seed_of, pair_of, kRejectCap};
     const dim3 grid((unsigned)gx, (unsigned)chunks);
     const uint64_t r64 = lazy ? (UINT64_MAX % mm + 1) % mm : 0;          // 2^64 mod m
-#define SDA_CHACHA_LAUNCH(L, DI)                                                                          \
-    hipLaunchKernelGGL((chacha_combine_kernel<L, DI>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds, per, D, \
-                       dst, M, zone, r64, log)
+    // round 1's uniform columns per seed, once (every block counter's high word is 0 below 2^32 blocks)
+    ChachaPre* pre = reinterpret_cast<ChachaPre*>(base + chacha_pre_off(D));
+    const bool use_pre = !secrets && n_seeds && n_blk <= (1ull << 32);
+    if (use_pre) {
+        hipLaunchKernelGGL(chacha_pre_kernel, dim3((unsigned)((n_seeds + 255) / 256)), dim3(256), 0, s, seeds_dev, w,
+                           n_seeds, pre);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+#define SDA_CHACHA_LAUNCH(L, DI)                                                                              \
+    do {                                                                                                      \
+        if (use_pre)                                                                                          \
+            hipLaunchKernelGGL((chacha_combine_kernel<L, DI, true>), grid, dim3(256), 0, s, seeds_dev, w,     \
+                               n_seeds, per, D, dst, M, zone, r64, log, (const ChachaPre*)pre);               \
+        else                                                                                                  \
+            hipLaunchKernelGGL((chacha_combine_kernel<L, DI>), grid, dim3(256), 0, s, seeds_dev, w, n_seeds,  \
+                               per, D, dst, M, zone, r64, log, (const ChachaPre*)nullptr);                    \
+    } while (0)
     const bool small_m = mm <= (1ull << 62);
     if (secrets)
         hipLaunchKernelGGL(chacha_mask_add_kernel, dim3((unsigned)gx), dim3(256), 0, s, seeds_dev, w, D, dst, M, zone,

@@ -194,7 +194,7 @@ sda_status chacha_combine(sda_engine* h, int64_t m, uint64_t D, const uint32_t* 
     // compare them at sizes the oracle cannot finish)
     const char* force = getenv("SDA_CHACHA_PATH");
     if (!sda::chacha_needs_stream_path(m) && !(force && strcmp(force, "stream") == 0)) {
-        if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D))) return e;
+        if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D, n))) return e;
         bool overflow = false;
         int fixups = 0;
         HIP_TRY(sda::launch_chacha_mask_combine(m, D, seeds, w, n, out, h->work, st, &overflow, &fixups));
@@ -225,7 +225,7 @@ sda_status chacha_combine_begin(sda_engine* h, int64_t m, uint64_t D, const uint
     const char* force = getenv("SDA_CHACHA_PATH");
     if (sda::chacha_needs_stream_path(m) || (force && strcmp(force, "stream") == 0) || n == 0)
         return chacha_combine(h, m, D, seeds, w, n, out, st);
-    if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D))) return e;
+    if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D, n))) return e;
     HIP_TRY(sda::launch_chacha_mask_combine_async(m, D, seeds, w, n, out, h->work, st, h->rej_host));
     *pc = PendingChacha{true, m, D, n, seeds, w, out};
     return SDA_OK;
@@ -1358,7 +1358,7 @@ sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms
             // chacha.rs:36-45: masked = (secrets + draw) % m over one stream
             const char* force = getenv("SDA_CHACHA_PATH");
             if (!sda::chacha_needs_stream_path(ms->modulus) && !(force && strcmp(force, "stream") == 0)) {
-                if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D))) return e;
+                if (sda_status e = ensure(&h->work, &h->work_bytes, sda::chacha_work_bytes(D, 0))) return e;
                 HIP_TRY(sda::launch_chacha_mask_add_async(ms->modulus, D, dseed, w, secrets, dm, h->work, st,
                                                           h->rej_host));
                 mask_pending = true;

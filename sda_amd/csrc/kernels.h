@@ -163,12 +163,12 @@ hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len
 // ---- chacha.hip ----
 // Combine of n_seeds ChaCha mask streams (chacha.rs:57-76), two implementations:
 //  * fast path: counter mode, canonical sums, rejections logged and fixed up.  `work` must hold
-//    chacha_work_bytes(D).  Valid when !chacha_needs_stream_path(m); sets *overflow (and writes
+//    chacha_work_bytes(D, n_seeds).  Valid when !chacha_needs_stream_path(m); sets *overflow (and writes
 //    nothing) when more rejections occur than its log holds -- rerun on the stream path.
 //  * stream path: the draws of a tile of streams expanded exactly (any rejection rate) into rows,
 //    then the exact sequential combine recurrence (wrapping i64 add for m > 2^62, as the reference).
 //    `work` must hold chacha_stream_work_bytes(D, n_seeds, m).  Host-synchronous per tile.
-size_t chacha_work_bytes(uint64_t dimension);
+size_t chacha_work_bytes(uint64_t dimension, uint64_t n_seeds);
 bool chacha_needs_stream_path(int64_t modulus);
 size_t chacha_stream_work_bytes(uint64_t dimension, uint64_t n_seeds, int64_t modulus);
 hipError_t launch_chacha_mask_combine(int64_t modulus, uint64_t dimension, const uint32_t* seeds,
