@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 A/B: the clerk's slot combine with 16 blobs' slot loads in flight per lane (SDA_SLOT_UNROLL=16)
+# Round-3 A/B (knob removed after it, profiles/r03t): the clerk's slot combine with 16 blobs' slot loads in flight per lane (SDA_SLOT_UNROLL=16)
 # vs 8 (the default), interleaved, on the codec leg (1000 x 1M varint payloads); codec tests first.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

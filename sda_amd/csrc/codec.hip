@@ -1208,12 +1208,6 @@ static uint32_t slot_cpl() {
     return (v == 1 || v == 2) ? (uint32_t)v : 4u;
 }
 
-// blobs whose slot loads a lane issues before their dependent adds (A/B knob SDA_SLOT_UNROLL = 8 | 16)
-static uint32_t slot_unroll() {
-    const char* e = getenv("SDA_SLOT_UNROLL");
-    return (e && atoi(e) == 16) ? 16u : 8u;
-}
-
 size_t varint_slot_bytes(const VarintPlan& plan, uint64_t n_blobs, uint64_t dim) {
     const uint64_t ntiles = (dim + kThreads - 1) / kThreads;          // plan room for the smallest tile
     return (plan.regions * kSlotCap + (kRegionBytes - kSlotCap)) * sizeof(int32_t) + ntiles * n_blobs * 8 + 256;
@@ -1259,16 +1253,9 @@ hipError_t launch_varint_decode_slots_combine(const uint8_t* bytes, const uint64
         const Mod64 M = make_mod64(modulus);
         const bool small_m = modulus <= ((int64_t)1 << 62);
         const dim3 g((unsigned)ntiles), blk(kThreads);
-        const bool u16 = slot_unroll() == 16;
-#define SLOT_LAUNCH(C, SM)                                                                                      \
-    do {                                                                                                        \
-        if (u16)                                                                                                \
-            hipLaunchKernelGGL((slot_combine_kernel<C, 16, SM>), g, blk, 0, s, slots, (const uint64_t*)tplan,    \
-                               n_blobs, (const uint64_t*)w.blob_count, (const uint32_t*)w.wide, out_cap, out, M); \
-        else                                                                                                    \
-            hipLaunchKernelGGL((slot_combine_kernel<C, 8, SM>), g, blk, 0, s, slots, (const uint64_t*)tplan,     \
-                               n_blobs, (const uint64_t*)w.blob_count, (const uint32_t*)w.wide, out_cap, out, M); \
-    } while (0)
+#define SLOT_LAUNCH(C, SM)                                                                                 \
+    hipLaunchKernelGGL((slot_combine_kernel<C, 8, SM>), g, blk, 0, s, slots, (const uint64_t*)tplan, n_blobs, \
+                       (const uint64_t*)w.blob_count, (const uint32_t*)w.wide, out_cap, out, M)
         if (cpl == 4) { if (small_m) SLOT_LAUNCH(4, true); else SLOT_LAUNCH(4, false); }
         else if (cpl == 2) { if (small_m) SLOT_LAUNCH(2, true); else SLOT_LAUNCH(2, false); }
         else { if (small_m) SLOT_LAUNCH(1, true); else SLOT_LAUNCH(1, false); }
