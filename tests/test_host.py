@@ -169,6 +169,12 @@ def test_gloo_mask_reduce_and_column_split(world):
         assert got == exp, k
 
 
+def test_exchange_at_world1_is_off_by_default():
+    """The forced one-rank exchange is a test hook: product callers at world size 1 never run a collective."""
+    assert Dd.EXCHANGE_AT_WORLD_1 is False
+    assert not Dd._exchange(1) and Dd._exchange(2)
+
+
 def test_world1_helpers_return_exact_signed_result():
     """At world size 1 no reduce runs: the exact single-pass result is returned unchanged, signed
     values included (no canonicalising finalize)."""
