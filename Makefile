@@ -16,7 +16,7 @@ PLAIN   := combine elementwise chacha codec snapshot packed_wide
 OBJS    := $(patsubst %,$(OBJDIR)/%.o,$(PLAIN)) $(OBJDIR)/engine.o \
            $(OBJDIR)/packed_gen.o $(patsubst %,$(OBJDIR)/packed_gen_%.o,$(GEN_PARTS)) \
            $(OBJDIR)/packed_reveal.o $(patsubst %,$(OBJDIR)/packed_reveal_%.o,$(REVEAL_PARTS))
-HDRS    := $(CSRC)/packed_common.h $(CSRC)/kernels.h $(CSRC)/modarith.h include/sda_engine.h
+HDRS    := $(CSRC)/packed_common.h $(CSRC)/kernels.h $(CSRC)/modarith.h $(CSRC)/xcd.h include/sda_engine.h
 
 all: $(LIB) oracle
 

@@ -68,7 +68,10 @@ struct PackedGenArgs {
     bool canonical = false;       // shares as canonical residues in [0, p) instead of tss' signed values
     uint32_t prime = 0;           // set by launch_packed_generate (selects the lazy-truncation kernel)
     bool signbit = false;         // set by launch_packed_generate (sign-bit radix-2 half, packed_gen.hip)
+    bool xcd_order = true;        // set by launch_packed_generate: XCD-chunked tile order (xcd.h)
 };
+// A/B knob: SDA_XCD_ORDER=0 runs the streaming kernels in natural workgroup order (xcd.h).
+bool xcd_order_enabled();
 // Exact share-gen uses lazy truncation (packed_gen.hip: Trunc<true>) for primes at least this big.
 constexpr uint32_t kLazyTruncMinP = 1u << 24;
 // Batches whose inputs fall outside (-p, p) are logged by the fast kernel and recomputed by a

@@ -2,6 +2,7 @@
 #include <stdlib.h>
 
 #include "packed_common.h"
+#include "xcd.h"
 
 namespace sda {
 using namespace packed;
@@ -188,7 +189,8 @@ __device__ __forceinline__ void transform_canon(const int64_t (&raw)[L], const G
     static_for<0, N3>([&](auto j) { ys[j] = (int32_t)y[j]; });
 }
 
-// One workgroup = one tile (vector blockIdx.y, BS batches from blockIdx.x * BS).
+// One workgroup = one tile: vector lin / gridDim.x, BS batches from (lin % gridDim.x) * BS, where lin is
+// the XCD-chunked linear workgroup id (xcd.h).
 //
 // Lane -> batch map: lane i < 32 takes batch 2i of its wave's 64, lane 32 + i batch 2i + 1.  After
 // the transform one v_permlane32_swap per pair of clerk rows leaves lane i holding batches
@@ -201,7 +203,7 @@ __global__ __launch_bounds__(gen_block<L>())
 __attribute__((amdgpu_waves_per_eu(gen_waves<L, CANON, LAZY>(), gen_waves<L, CANON, LAZY>())))
 void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const int64_t* __restrict__ draws,
                        int64_t* __restrict__ out, uint32_t k, uint32_t t, uint64_t B,
-                       const GenTables* __restrict__ Tp, unsigned int* __restrict__ log) {
+                       const GenTables* __restrict__ Tp, unsigned int* __restrict__ log, int xcd) {
     constexpr int LB = ilog(L, 2);
     constexpr int ND = ilog(N3, 3);
     constexpr int BS = gen_block<L>();
@@ -223,8 +225,10 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
 
     {
         const GenTables& T = *Tp;
-        const uint32_t vec = blockIdx.y;
-        const uint64_t b0 = (uint64_t)blockIdx.x * BS;
+        // XCD-chunked tile order (xcd.h): each XCD streams one contiguous eighth of the [vector][tile] grid
+        const uint64_t lin = xcd ? xcd_linear_block() : blockIdx.x + (uint64_t)blockIdx.y * gridDim.x;
+        const uint32_t vec = (uint32_t)(lin / gridDim.x);
+        const uint64_t b0 = (lin % gridDim.x) * BS;
         const int64_t* sec = secrets + (uint64_t)vec * D;
 
         // ---- stage the tile's inputs through LDS with coalesced loads ----
@@ -444,8 +448,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                 if (live) {
                     const uint32_t slot = atomicAdd(log, 1u);
                     if (slot < kGenLogCap)
-                        reinterpret_cast<uint64_t*>(log + 16)[slot] =
-                            (uint64_t)blockIdx.y * B + (uint64_t)blockIdx.x * BS + lb;
+                        reinterpret_cast<uint64_t*>(log + 16)[slot] = (uint64_t)vec * B + b0 + lb;
                 }
             }
         }
@@ -481,18 +484,19 @@ static void gen_launch_mode(const PackedGenArgs& a, uint32_t k, uint32_t t, uint
     constexpr int BS = gen_block<L>();
     const dim3 grid((unsigned)((B + BS - 1) / BS), (unsigned)a.n_vectors);
     const bool wide = B % 2 == 0 && ((uintptr_t)a.out % 16) == 0;
+    const int xcd = a.xcd_order ? 1 : 0;
     if (wide && !CANON && p >= kLazyTruncMinP && a.signbit)   // exact shares, sign-bit radix-2 half
         hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, false, true, true>), grid, dim3(BS), 0, s, a.secrets,
-                           a.dimension, a.draws, a.out, k, t, B, T, log.count);
+                           a.dimension, a.draws, a.out, k, t, B, T, log.count, xcd);
     else if (wide && !CANON && p >= kLazyTruncMinP)          // exact shares, lazy zero handling
         hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, false, true>), grid, dim3(BS), 0, s, a.secrets,
-                           a.dimension, a.draws, a.out, k, t, B, T, log.count);
+                           a.dimension, a.draws, a.out, k, t, B, T, log.count, xcd);
     else if (wide)
         hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, CANON, false>), grid, dim3(BS), 0, s, a.secrets,
-                           a.dimension, a.draws, a.out, k, t, B, T, log.count);
+                           a.dimension, a.draws, a.out, k, t, B, T, log.count, xcd);
     else
         hipLaunchKernelGGL((packed_gen_kernel<L, N3, false, CANON, false>), grid, dim3(BS), 0, s, a.secrets,
-                           a.dimension, a.draws, a.out, k, t, B, T, log.count);
+                           a.dimension, a.draws, a.out, k, t, B, T, log.count, xcd);
 }
 
 template <int L, int N3>
@@ -608,6 +612,14 @@ __global__ __launch_bounds__(64) void packed_gen_fixup_kernel(const int64_t* __r
 
 }  // namespace
 
+bool xcd_order_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("SDA_XCD_ORDER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 size_t packed_gen_log_bytes() { return 64 + (size_t)kGenLogCap * sizeof(uint64_t); }
 
 hipError_t launch_packed_generate(const PackedGenArgs& args, uint32_t k, uint32_t t, uint32_t n, uint32_t p,
@@ -632,6 +644,7 @@ hipError_t launch_packed_generate(const PackedGenArgs& args, uint32_t k, uint32_
     }
     const char* sb = getenv("SDA_GEN_SIGNBIT");                 // A/B knob: 0 = the mad_i64 sign kernel
     a.signbit = (tab.flags & 1u) && !(sb && sb[0] == '0');
+    a.xcd_order = xcd_order_enabled();
     const GenTables* T = static_cast<const GenTables*>(tab.dev);
     GenFixupLog log{static_cast<unsigned int*>(log_buf),
                     reinterpret_cast<uint64_t*>(static_cast<unsigned int*>(log_buf) + 16), kGenLogCap};

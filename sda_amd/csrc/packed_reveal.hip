@@ -1,5 +1,6 @@
 // packed_reveal.hip -- packed-Shamir reveal, EXACT (Newton) and CANONICAL (Lagrange).
 #include "packed_common.h"
+#include "xcd.h"
 
 namespace sda {
 using namespace packed;
@@ -225,12 +226,14 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
                                                                   uint64_t D, int64_t* __restrict__ out,
                                                                   uint32_t n_idx, uint32_t k,
                                                                   const uint32_t* __restrict__ tab, MontP M,
-                                                                  unsigned int* __restrict__ log) {
+                                                                  unsigned int* __restrict__ log, int xcd) {
     extern __shared__ int64_t lds_o[];
     const uint32_t tid = threadIdx.x;
-    const uint64_t b0 = (uint64_t)blockIdx.x * 256, b = b0 + tid;
+    // XCD-chunked tile order (xcd.h)
+    const uint64_t lin = xcd ? xcd_linear_block() : blockIdx.x + (uint64_t)blockIdx.y * gridDim.x;
+    const uint64_t b0 = (lin % gridDim.x) * 256, b = b0 + tid;
     const bool live = b < B;
-    const uint64_t vec = blockIdx.y;
+    const uint64_t vec = lin / gridDim.x;
     const int64_t* sh = shares + vec * (uint64_t)n_idx * B + (live ? b : B - 1);
     int64_t* o = out + vec * D;
     const uint32_t m = FULL ? (uint32_t)MMAX : n_idx + 1;
@@ -396,12 +399,13 @@ template <int NMAX, bool STAGED>
 __global__ __launch_bounds__(256) void packed_reveal_canon_kernel(const int64_t* __restrict__ shares, uint64_t B,
                                                                   uint64_t D, int64_t* __restrict__ out,
                                                                   uint32_t n_idx, uint32_t k,
-                                                                  const uint32_t* __restrict__ tab, MontP M) {
+                                                                  const uint32_t* __restrict__ tab, MontP M, int xcd) {
     extern __shared__ int64_t lds_o[];
     const uint32_t tid = threadIdx.x;
-    const uint64_t b0 = (uint64_t)blockIdx.x * 256, b = b0 + tid;
+    const uint64_t lin = xcd ? xcd_linear_block() : blockIdx.x + (uint64_t)blockIdx.y * gridDim.x;
+    const uint64_t b0 = (lin % gridDim.x) * 256, b = b0 + tid;
     const bool live = b < B;
-    const uint64_t vec = blockIdx.y;
+    const uint64_t vec = lin / gridDim.x;
     const int64_t* sh = shares + vec * (uint64_t)n_idx * B + (live ? b : B - 1);
     int64_t* o = out + vec * D;
     const uint32_t p = M.p;
@@ -453,27 +457,28 @@ hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32
     dim3 grid((unsigned)((B + 255) / 256), (unsigned)a.n_vectors);
     const bool staged = k <= 16;                      // LDS stage: 256 * k * 8 B <= 32 KiB
     const size_t lds = staged ? (size_t)256 * k * sizeof(int64_t) : 0;
+    const int xcd = xcd_order_enabled() ? 1 : 0;
     if (mode == 0) {
         bool done = false;
         if constexpr (MM <= 16) {
             done = staged && k <= 8;
             if (done && M.p >= kLazyTruncMinP && n_idx + 1 == MM)
                 hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, true, true>), grid, dim3(256), lds, s,
-                                   a.shares, B, a.dimension, a.out, n_idx, k, tab, M, log);
+                                   a.shares, B, a.dimension, a.out, n_idx, k, tab, M, log, xcd);
             else if (done && M.p >= kLazyTruncMinP)
                 hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, true>), grid, dim3(256), lds, s,
-                                   a.shares, B, a.dimension, a.out, n_idx, k, tab, M, log);
+                                   a.shares, B, a.dimension, a.out, n_idx, k, tab, M, log, xcd);
             else if (done)
                 hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, false>), grid, dim3(256), lds, s,
-                                   a.shares, B, a.dimension, a.out, n_idx, k, tab, M, log);
+                                   a.shares, B, a.dimension, a.out, n_idx, k, tab, M, log, xcd);
         }
         if (done) {
         } else if (staged) {
             hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 0, false>), grid, dim3(256), lds, s, a.shares,
-                               B, a.dimension, a.out, n_idx, k, tab, M, log);
+                               B, a.dimension, a.out, n_idx, k, tab, M, log, xcd);
         } else {
             hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, false, 0, false>), grid, dim3(256), 0, s, a.shares,
-                               B, a.dimension, a.out, n_idx, k, tab, M, log);
+                               B, a.dimension, a.out, n_idx, k, tab, M, log, xcd);
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -490,10 +495,10 @@ hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32
     } else {
         if (staged)
             hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, true>), grid, dim3(256), lds, s, a.shares, B,
-                               a.dimension, a.out, n_idx, k, tab, M);
+                               a.dimension, a.out, n_idx, k, tab, M, xcd);
         else
             hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, false>), grid, dim3(256), 0, s, a.shares, B,
-                               a.dimension, a.out, n_idx, k, tab, M);
+                               a.dimension, a.out, n_idx, k, tab, M, xcd);
     }
     return hipGetLastError();
 }

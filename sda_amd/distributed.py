@@ -11,7 +11,10 @@ ranks' results:
 
 * no negative input anywhere: the int64 SUM of the ranks' canonical results, taken by that ONE
   all-reduce over RCCL (xGMI), then a device `% m` (sda_combine_finalize_dev), IS the reference's
-  result.  Overflow headroom (proved before the reduce): |sum| <= G (m - 1) <= 2^63 - 1.
+  result.  Overflow headroom (proved before the reduce): |sum| <= G (m - 1) <= 2^63 - 1.  The step
+  queues pass 1, the all-reduce and the finalize back to back with no host read between them; the two
+  flags reach the host by an asynchronous copy that SplitTicket.finish() checks afterwards (at the end
+  of the call, or later with defer=True), and only a flagged job does more work.
 * some negative input: exact two-pass split (SURVEY §7 hard part 1 option (b)).  The
   pass-1 results are all-gathered; each rank g > 0 gets its incoming residue c_in = canonical sum of
   ranks < g and replays its rows from c_in, recording only the LAST sign event (set / reset / none) of
@@ -106,51 +109,76 @@ class SplitStats:
     """What the last participation split did on this rank (bench.py and the tests read it)."""
     signed = False      # some rank saw a negative input -> the two-pass path ran
     passes = 1
+    world = 1           # ranks in the group the split ran over
+    redo_pass1 = False  # the two-pass path recomputed pass 1 (its buffer was reused before finish())
 
 
-def _combine_split(engine, modulus: int, tiles, dim: int, row_stride: int, partial, out, group, stream,
-                   stats: SplitStats = None):
-    """The participation split of combiner.rs:16-28 (module doc): this rank's rows as row tiles
-    [(ptr, n_rows), ...] in participation order; `partial` int64 [dim] receives this rank's pass-1
-    result, `out` int64 [dim] the job's result on every rank."""
+# Per (device, dim, stream) exchange buffer [dim results | 2 flags], kept across calls: a step allocates
+# nothing.  Calls on one stream are ordered by the stream, so one buffer per stream is race-free.
+_WORK = {}
+# partial buffer -> generation of the last pass 1 written into it (a deferred ticket's pass-1 result is
+# still there only if no later split wrote the same buffer)
+_GEN = {}
+
+
+def _workspace(t, dim: int, st):
     import torch
-    import torch.distributed as dist
+    key = (str(t.device), dim, st)
+    w = _WORK.get(key)
+    if w is None:
+        if len(_WORK) > 16:
+            _WORK.clear()
+        w = _WORK[key] = torch.empty(dim + 2, dtype=torch.int64, device=t.device)
+    return w
 
-    tiles = list(tiles)
-    world = _world(group)
-    st = _stream(partial, stream)
-    stats = stats if stats is not None else SplitStats()
-    stats.signed, stats.passes = False, 1
-    with _on(partial, st):
-        if not _exchange(world):     # one sequential pass: the exact result, signed values included
-            if len(tiles) == 1:
-                engine.combine_dev(modulus, tiles[0][0], tiles[0][1], dim, row_stride, partial.data_ptr(), st)
-            else:
-                partial.zero_()
-                for ptr, n in tiles:
-                    engine.combine_accumulate_dev(modulus, ptr, n, dim, row_stride, partial.data_ptr(), st)
-            out.copy_(partial)
+
+class SplitTicket:
+    """A participation-split step whose sign flags are still in flight (module doc; the pattern of the
+    engine's chacha_combine_begin/_end).  The step has already ENQUEUED everything the non-negative case
+    needs -- pass 1, the one all-reduce, the finalize into `out` -- and an asynchronous copy of the two
+    all-reduced flags into pinned host memory.  finish() waits for that 16-byte copy only, then:
+    risk flag -> ValueError; negative flag -> the exact two-pass split, which rewrites `out`.
+    `out` holds the job's result once finish() has returned.  Every rank must call finish() (the signed
+    path runs collectives), in the same order relative to its other collectives.  Idempotent."""
+
+    def __init__(self, engine, modulus, tiles, dim, row_stride, partial, out, group, st, stats, flags_h, event,
+                 gen):
+        self._args = (engine, modulus, tiles, dim, row_stride, partial, out, group, st, stats)
+        self._flags_h, self._event, self._gen = flags_h, event, gen
+        self._finished = False
+
+    def done(self) -> bool:
+        """True once the flags have landed on the host (finish() will not block)."""
+        return self._event is None or self._event.query()
+
+    def finish(self) -> None:
+        if self._finished:
             return
-        partial.zero_()
-        if not reduce_headroom_ok(world, modulus):
-            raise ValueError(f"reduce headroom: {world} * (m - 1) exceeds 2^63 - 1")
-        rank = dist.get_rank(group)
-        # pass 1 + the flags, then ONE all-reduce of [partial | flags]
-        work = torch.zeros(dim + 2, dtype=torch.int64, device=partial.device)
-        for ptr, n in tiles:
-            engine.combine_split_dev(modulus, ptr, n, dim, row_stride, partial.data_ptr(),
-                                     work[dim:].data_ptr(), st)
-        work[:dim].copy_(partial)
-        dist.all_reduce(work, op=dist.ReduceOp.SUM, group=group)
-        neg, risk = (int(v) for v in work[dim:].tolist())          # host sync: 16 bytes
+        self._finished = True
+        if self._event is not None:
+            self._event.synchronize()             # the 16-byte flag copy, queued after the finalize
+        neg, risk = int(self._flags_h[0]), int(self._flags_h[1])
         if risk:
             raise ValueError("participation split: an input lies outside [-(2^63 - m), 2^63 - m], where the "
                              "reference's running sum may wrap; combine on one rank or split by columns")
-        if not neg:
-            engine.combine_finalize_dev(modulus, work.data_ptr(), dim, out.data_ptr(), st)
-            return
-        # signed inputs: the exact two-pass split
-        stats.signed, stats.passes = True, 2
+        if neg:
+            _two_pass(*self._args, redo=_GEN.get(self._args[5].data_ptr()) != self._gen)
+
+
+def _two_pass(engine, modulus, tiles, dim, row_stride, partial, out, group, st, stats, redo):
+    """Signed inputs somewhere: the exact two-pass split (module doc).  `partial` holds this rank's pass-1
+    result unless `redo` (a later split reused the buffer before a deferred finish()): pass 1 again."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank = _world(group), dist.get_rank(group)
+    stats.signed, stats.passes, stats.redo_pass1 = True, 3 if redo else 2, redo
+    with _on(partial, st):
+        if redo:                     # into a scratch buffer: `partial` may hold a later ticket's pass 1
+            flags = torch.zeros(2, dtype=torch.int64, device=partial.device)
+            partial = torch.zeros(dim, dtype=torch.int64, device=partial.device)
+            for ptr, n in tiles:
+                engine.combine_split_dev(modulus, ptr, n, dim, row_stride, partial.data_ptr(), flags.data_ptr(), st)
         gathered = torch.empty((world, dim), dtype=torch.int64, device=partial.device)
         dist.all_gather(list(gathered.unbind(0)), partial, group=group)
         state = torch.empty(dim, dtype=torch.int64, device=partial.device)
@@ -166,19 +194,81 @@ def _combine_split(engine, modulus: int, tiles, dim: int, row_stride: int, parti
         engine.combine_split_resolve_dev(modulus, total.data_ptr(), code.data_ptr(), dim, out.data_ptr(), st)
 
 
+def _combine_split(engine, modulus: int, tiles, dim: int, row_stride: int, partial, out, group, stream,
+                   stats: SplitStats = None, defer: bool = False):
+    """The participation split of combiner.rs:16-28 (module doc): this rank's rows as row tiles
+    [(ptr, n_rows), ...] in participation order; `partial` int64 [dim] receives this rank's pass-1
+    result, `out` int64 [dim] the job's result on every rank.  The non-negative case makes no blocking
+    host read: pass 1, the all-reduce and the finalize are queued back to back and the flags travel
+    to the host asynchronously (SplitTicket).  defer=False checks them before returning (after all
+    the work is queued); defer=True returns the ticket and the caller finishes it later."""
+    import torch
+    import torch.distributed as dist
+
+    tiles = list(tiles)
+    world = _world(group)
+    st = _stream(partial, stream)
+    stats = stats if stats is not None else SplitStats()
+    stats.signed, stats.passes, stats.world, stats.redo_pass1 = False, 1, world, False
+    with _on(partial, st):
+        if not _exchange(world):     # one sequential pass: the exact result, signed values included
+            if len(tiles) == 1:
+                engine.combine_dev(modulus, tiles[0][0], tiles[0][1], dim, row_stride, partial.data_ptr(), st)
+            else:
+                partial.zero_()
+                for ptr, n in tiles:
+                    engine.combine_accumulate_dev(modulus, ptr, n, dim, row_stride, partial.data_ptr(), st)
+            out.copy_(partial)
+            return None
+        if not reduce_headroom_ok(world, modulus):
+            raise ValueError(f"reduce headroom: {world} * (m - 1) exceeds 2^63 - 1")
+        # pass 1 into `partial` (kept for the signed path) + the flags, then ONE all-reduce of
+        # [results | flags] in the cached exchange buffer
+        work = _workspace(partial, dim, st)
+        partial.zero_()
+        work[dim:].zero_()
+        for ptr, n in tiles:
+            engine.combine_split_dev(modulus, ptr, n, dim, row_stride, partial.data_ptr(),
+                                     work[dim:].data_ptr(), st)
+        if len(_GEN) > 1024:
+            _GEN.clear()
+        gen = _GEN[partial.data_ptr()] = _GEN.get(partial.data_ptr(), 0) + 1
+        work[:dim].copy_(partial)
+        dist.all_reduce(work, op=dist.ReduceOp.SUM, group=group)
+        # the finalize is the result whenever no rank saw a negative input: queue it now, read the
+        # flags later (a signed job rewrites `out` in finish())
+        engine.combine_finalize_dev(modulus, work.data_ptr(), dim, out.data_ptr(), st)
+        if work.is_cuda:
+            flags_h = torch.empty(2, dtype=torch.int64, pin_memory=True)
+            flags_h.copy_(work[dim:], non_blocking=True)
+            event = torch.cuda.Event()
+            event.record()                       # on `st` (the current stream inside _on)
+        else:                                    # host tensors (CPU / gloo tests): already there
+            flags_h, event = work[dim:].clone(), None
+    ticket = SplitTicket(engine, modulus, tiles, dim, row_stride, partial, out, group, st, stats, flags_h, event,
+                         gen)
+    if defer:
+        return ticket
+    ticket.finish()
+    return None
+
+
 def combine_tiles_sharded(engine, modulus: int, tiles: Iterable[Tuple[int, int]], dim: int, row_stride: int,
-                          partial, out, group=None, stream=None, stats: SplitStats = None):
+                          partial, out, group=None, stream=None, stats: SplitStats = None, defer: bool = False):
     """This rank's participations as row tiles [(shares_ptr, n_rows), ...] (the recurrence continues
     across tiles, so they act as one pass; the signed path reads them twice) through the exact
     participation split.  `partial` / `out`: int64 [dim] on this rank's device.  Any inputs: signed
-    ones take the two-pass path; inputs the reference's sum could wrap on raise ValueError."""
-    _combine_split(engine, modulus, tiles, dim, row_stride, partial, out, group, stream, stats)
+    ones take the two-pass path; inputs the reference's sum could wrap on raise ValueError.
+    defer=True returns a SplitTicket (N > 1; None at world size 1): `out` is final after its finish()."""
+    return _combine_split(engine, modulus, tiles, dim, row_stride, partial, out, group, stream, stats, defer)
 
 
 def combine_rows_sharded(engine, modulus: int, shares_ptr: int, n_local: int, dim: int, row_stride: int,
-                         partial, out, group=None, stream=None, stats: SplitStats = None):
-    """Exact participation split of combiner.rs:16-28 over this rank's [n_local][row_stride] rows."""
-    _combine_split(engine, modulus, [(shares_ptr, n_local)], dim, row_stride, partial, out, group, stream, stats)
+                         partial, out, group=None, stream=None, stats: SplitStats = None, defer: bool = False):
+    """Exact participation split of combiner.rs:16-28 over this rank's [n_local][row_stride] rows
+    (defer: see combine_tiles_sharded)."""
+    return _combine_split(engine, modulus, [(shares_ptr, n_local)], dim, row_stride, partial, out, group, stream,
+                          stats, defer)
 
 
 def mask_combine_sharded(engine, modulus: int, dim: int, seeds, partial, out, group=None, stream=None):

@@ -98,6 +98,25 @@ def _worker_rows(rank, world, port, q):
         calls = [None] * world
         dist.all_gather_object(calls, sorted(set(eng.calls)))
         res[name + "/calls"] = sorted(set(c for cs in calls for c in cs))
+    # deferred tickets (defer=True): a non-negative job, whose result is final once finish() has read the
+    # flags, then two signed jobs through ONE partial buffer before either is finished -- the first signed
+    # ticket's pass-1 result was overwritten, so its finish() recomputes pass 1
+    m, D = 2147482801, 77
+    jobs = [synth.fill(19, D, 0x5DA + 40 + j, lo, m) for j, lo in enumerate((0, -(m - 1), -(m - 1)))]
+    part = torch.empty(D, dtype=torch.int64)
+    outs, tickets, stats = [], [], []
+    for x in jobs:
+        start, count = Dd.shard_range(x.shape[0], rank, world)
+        mine = torch.from_numpy(x[start:start + count].copy())
+        outs.append(torch.empty(D, dtype=torch.int64))
+        stats.append(Dd.SplitStats())
+        tickets.append((Dd.combine_rows_sharded(CpuEngine(), m, mine.data_ptr(), count, D, D, part, outs[-1],
+                                                stats=stats[-1], defer=True), mine))
+    for t, _ in tickets:
+        t.finish()
+        t.finish()                                   # idempotent
+    res["deferred"] = [(o.tolist(), O.combine(m, x).tolist(), s.signed, s.redo_pass1, s.passes)
+                       for o, x, s in zip(outs, jobs, stats)]
     # an input the reference's running sum could wrap on: the split refuses it (never a wrong value)
     m = 1000003
     x = torch.from_numpy(synth.fill(4, 8, 1, 0, 100))
@@ -122,6 +141,11 @@ def test_gloo_sharded_combine_matches_single_pass(world):
     inputs where the reference's own sum may wrap."""
     res = _run_world2(_worker_rows, world)
     assert res.pop("wrap_refused") is True
+    deferred = res.pop("deferred")
+    for got, exp, *_ in deferred:
+        assert got == exp
+    # (signed, pass 1 recomputed, passes): the second job's buffer was reused by the third before its finish()
+    assert [tuple(d[2:]) for d in deferred] == [(False, False, 1), (True, True, 3), (True, False, 2)]
     split = ["combine_finalize_dev", "combine_split_dev"]
     two_pass = ["combine_split_dev", "combine_split_prefix_dev", "combine_split_replay_dev",
                 "combine_split_resolve_dev"]
@@ -131,7 +155,9 @@ def test_gloo_sharded_combine_matches_single_pass(world):
             assert got == exp, (name, kind)
             assert signed == (name != "nonneg"), (name, kind)
         calls = res[name + "/calls"]
-        exp_calls = split if name == "nonneg" else [c for c in two_pass if world > 1 or "replay" not in c]
+        # the finalize is queued before the flags are read, so signed jobs run it too (then resolve)
+        exp_calls = split if name == "nonneg" else sorted(set(split) | {c for c in two_pass
+                                                                         if world > 1 or "replay" not in c})
         assert calls == exp_calls, (name, calls)           # (world 1 has no rank > 0 to replay)
 
 
