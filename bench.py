@@ -355,20 +355,33 @@ def main():
         # participations (row tiles for configs[3]), one int64 all-reduce over RCCL, device finalize
         tiles = [(shares.data_ptr(), min(tile, N - t0)) for t0 in range(0, N, tile)] if tile else None
 
+        # N > 1: each step's sign flags come back asynchronously (SplitTicket); a step finishes the
+        # PREVIOUS step's ticket after queueing its own work, so no host read sits between a step's
+        # all-reduce and its finalize, and the GPU never waits for the host
+        pending = []
+
         def step(timed):
             teng.timing = timed
             if tile:
-                Dd.combine_tiles_sharded(teng, m, tiles, D, D, partial, out)
+                t = Dd.combine_tiles_sharded(teng, m, tiles, D, D, partial, out, defer=True)
             else:
-                Dd.combine_rows_sharded(teng, m, shares.data_ptr(), N, D, D, partial, out)
+                t = Dd.combine_rows_sharded(teng, m, shares.data_ptr(), N, D, D, partial, out, defer=True)
+            while pending:
+                pending.pop().finish()
+            if t is not None:
+                pending.append(t)
 
         for _ in range(args.warmup):
             step(False)
+        while pending:
+            pending.pop().finish()
         torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step(True)
+        while pending:
+            pending.pop().finish()
         torch.cuda.synchronize()
         barrier()
         dt = time.perf_counter() - t0
@@ -741,9 +754,18 @@ def main():
         log(f"[pipelines] {json.dumps(side['pipelines'])}")
         del sec, drw, sh, pay, sub, out
 
+    dist_info = None
+    if world > 1:     # who took part: the driver's SCALE run can check that the communicator saw N ranks
+        props = torch.cuda.get_device_properties(local)
+        me = {"rank": rank, "local_rank": local, "device": local, "name": props.name,
+              "pci_bus_id": getattr(props, "pci_bus_id", None), "pci_device_id": getattr(props, "pci_device_id", None)}
+        allr = [None] * world
+        dist.all_gather_object(allr, me)
+        dist_info = {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "ranks": allr}
     if args.only is not None:
         return
     if rank == 0:
+        traffic = traffic_from_profile(tile if tile else N, D)
         rec = {
             "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
@@ -760,10 +782,12 @@ def main():
                        "exact": "combiner.rs:16-28 recurrence, bit-exact"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic_from_profile(tile if tile else N, D)},
+                         "traffic": traffic[0], "traffic_source": traffic[1]},
             "kernel_ms": round(kernel_ms, 4),
             "kernel_bytes_per_launch": bytes_per_launch,
         }
+        if dist_info is not None:
+            rec["dist"] = dist_info
         rec.update(side)
         if world == 1 and not args.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(min(D, 1_000_000), args.cpu_seconds)
@@ -913,17 +937,18 @@ def valu_roofline(key, ms, waves, blocks=None):
 
 
 def traffic_from_profile(N, D):
-    """HBM bytes per combine launch from the committed rocprofv3 PMC pass (profiles/), if it was
-    collected for this exact workload; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM."""
+    """(HBM bytes per combine launch, the profiles/ session they come from) from the committed rocprofv3
+    PMC pass, if it was collected for this exact workload; FETCH_SIZE doubled per MI355X_MICROARCH.md
+    §HBM.  (None, None) otherwise."""
     path = os.path.join(ROOT, "profiles", "combine_traffic.json")
     try:
         with open(path) as f:
             for t in json.load(f)["launches"]:
                 if t.get("rows") == N and t.get("dim") == D:
-                    return t["hbm_bytes_per_launch"]
+                    return t["hbm_bytes_per_launch"], t.get("source")
     except (OSError, ValueError, KeyError):
         pass
-    return None
+    return None, None
 
 
 if __name__ == "__main__":

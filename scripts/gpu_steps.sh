@@ -13,6 +13,7 @@
 #   trace[:<bench.py args>]      rocprofv3 --kernel-trace --stats over bench.py <args> -> trace/, kernel_stats_by_grid.csv
 #   pmc:<c1,c2,..>:<args>        one rocprofv3 --pmc pass over bench.py <args> -> pmc_<i>/ + summary
 #   tool:<binary> [args]         ./tools/<binary> [args]                    -> tool_<binary>.txt
+#   sh:<script> [args]           bash scripts/<script> [args]               -> sh_<i>.txt
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -79,6 +80,11 @@ for step in "$@"; do
         > "$T/pmc_$i.log" 2>&1 || { echo "pmc pass $i failed"; tail -5 "$T/pmc_$i.log"; exit 1; }
       python3 scripts/summarize_pmc.py "$T/pmc_$i" > "$T/pmc_$i.txt" 2>&1
       head -40 "$T/pmc_$i.txt"
+      ;;
+    sh)
+      # shellcheck disable=SC2086
+      timeout -k 10 900 bash scripts/$arg > "$T/sh_$i.txt" 2>&1 || { tail -20 "$T/sh_$i.txt"; exit 1; }
+      cat "$T/sh_$i.txt"
       ;;
     tool)
       bin=${arg%% *}

@@ -74,6 +74,43 @@ __device__ __forceinline__ void chacha_block_pre(const ChachaPre& P, const uint3
     o[12] = x12 + (uint32_t)counter; o[13] = x13 + (uint32_t)(counter >> 32); o[14] = x14; o[15] = x15;
 }
 
+// Two independent blocks (two seeds, same counter) with their quarter-rounds interleaved statement by
+// statement, so each dependent add -> xor -> rotate chain has a partner to issue beside it.
+#define SDA_QR2(a, b, c, d, A, B, C, D)                                        \
+    a += b; A += B; d ^= a; D ^= A; d = rotl(d, 16); D = rotl(D, 16);        \
+    c += d; C += D; b ^= c; B ^= C; b = rotl(b, 12); B = rotl(B, 12);        \
+    a += b; A += B; d ^= a; D ^= A; d = rotl(d, 8); D = rotl(D, 8);          \
+    c += d; C += D; b ^= c; B ^= C; b = rotl(b, 7); B = rotl(B, 7);
+
+__device__ __forceinline__ void chacha_block_pre_x2(const ChachaPre& P, const uint32_t* key, const ChachaPre& Q,
+                                                    const uint32_t* kq, uint64_t counter, uint32_t (&o)[16],
+                                                    uint32_t (&u)[16]) {
+    uint32_t x0 = C0, x4 = key[0], x8 = key[4], x12 = (uint32_t)counter;
+    uint32_t x1 = P.x1, x5 = P.x5, x9 = P.x9, x13 = P.x13, x2 = P.x2, x6 = P.x6, x10 = P.x10, x14 = P.x14;
+    uint32_t x3 = P.x3, x7 = P.x7, x11 = P.x11, x15 = P.x15;
+    uint32_t y0 = C0, y4 = kq[0], y8 = kq[4], y12 = (uint32_t)counter;
+    uint32_t y1 = Q.x1, y5 = Q.x5, y9 = Q.x9, y13 = Q.x13, y2 = Q.x2, y6 = Q.x6, y10 = Q.x10, y14 = Q.x14;
+    uint32_t y3 = Q.x3, y7 = Q.x7, y11 = Q.x11, y15 = Q.x15;
+    SDA_QR2(x0, x4, x8, x12, y0, y4, y8, y12);
+    SDA_QR2(x0, x5, x10, x15, y0, y5, y10, y15); SDA_QR2(x1, x6, x11, x12, y1, y6, y11, y12);
+    SDA_QR2(x2, x7, x8, x13, y2, y7, y8, y13); SDA_QR2(x3, x4, x9, x14, y3, y4, y9, y14);
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        SDA_QR2(x0, x4, x8, x12, y0, y4, y8, y12); SDA_QR2(x1, x5, x9, x13, y1, y5, y9, y13);
+        SDA_QR2(x2, x6, x10, x14, y2, y6, y10, y14); SDA_QR2(x3, x7, x11, x15, y3, y7, y11, y15);
+        SDA_QR2(x0, x5, x10, x15, y0, y5, y10, y15); SDA_QR2(x1, x6, x11, x12, y1, y6, y11, y12);
+        SDA_QR2(x2, x7, x8, x13, y2, y7, y8, y13); SDA_QR2(x3, x4, x9, x14, y3, y4, y9, y14);
+    }
+    o[0] = x0 + C0; o[1] = x1 + C1; o[2] = x2 + C2; o[3] = x3 + C3;
+    o[4] = x4 + key[0]; o[5] = x5 + key[1]; o[6] = x6 + key[2]; o[7] = x7 + key[3];
+    o[8] = x8 + key[4]; o[9] = x9 + key[5]; o[10] = x10 + key[6]; o[11] = x11 + key[7];
+    o[12] = x12 + (uint32_t)counter; o[13] = x13 + (uint32_t)(counter >> 32); o[14] = x14; o[15] = x15;
+    u[0] = y0 + C0; u[1] = y1 + C1; u[2] = y2 + C2; u[3] = y3 + C3;
+    u[4] = y4 + kq[0]; u[5] = y5 + kq[1]; u[6] = y6 + kq[2]; u[7] = y7 + kq[3];
+    u[8] = y8 + kq[4]; u[9] = y9 + kq[5]; u[10] = y10 + kq[6]; u[11] = y11 + kq[7];
+    u[12] = y12 + (uint32_t)counter; u[13] = y13 + (uint32_t)(counter >> 32); u[14] = y14; u[15] = y15;
+}
+
 // one ChaCha20 block: core(state) = rounds(state) + state
 __device__ __forceinline__ void chacha_block(const uint32_t* key, uint64_t counter, uint32_t (&o)[16]) {
     uint32_t x0 = C0, x1 = C1, x2 = C2, x3 = C3;
@@ -98,32 +135,28 @@ struct RejectLog {
     uint64_t cap;
 };
 
-// acc[i] += sum over seeds in this y-chunk of draw_i  (un-shifted), canonical per chunk.
-// Every draw is >= 0, so the reference's running `(r + draw) % m` equals (sum of draws) mod m.
-// LAZY (m <= 2^32): the raw 64-bit words v are summed into 96-bit accumulators (3 adds per draw)
-// and reduced once per chunk -- (sum of v) mod m == sum of (v mod m) mod m; otherwise each draw
-// is reduced with the 64-bit Barrett `%`.
 // A lane owns elements 8 blk .. 8 blk + 7; the workgroup's 2048 results go through LDS so that the
-// write-back is coalesced (lane t writes element t + 256 j): plain stores when the grid has a
-// single seed chunk (DIRECT: acc is the output), atomics into acc otherwise.
+// write-back is coalesced (lane t writes element t + 256 j).
 constexpr int kChachaPad = 9;                  // LDS row stride (u64) of a lane's 8 results
-// PRE: round 1's uniform columns of every seed come precomputed from `pre` (chacha_pre_kernel, counter
-// high word 0: the grid then holds < 2^32 blocks); otherwise the kernel computes them per seed.
-template <bool LAZY, bool DIRECT, bool PRE = false>
-__global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __restrict__ seeds, uint32_t w, uint64_t n_seeds,
-                           uint64_t seeds_per_chunk, uint64_t D, unsigned long long* __restrict__ acc, Mod64 M,
-                           uint64_t zone, uint64_t r64, RejectLog log, const ChachaPre* __restrict__ pre = nullptr) {
-    __shared__ unsigned long long st[256 * kChachaPad];
+#ifndef SDA_CHACHA_PAIR
+#define SDA_CHACHA_PAIR 0                      // build-time A/B knob: two interleaved seeds per step
+#endif
+// One tile (256 lanes x 8 draws = 2048 elements from tile x * 2048) over seeds [s0, s1): the lane's
+// canonical partial sums, written back through LDS (`st`) so that the stores are coalesced -- plain
+// stores when DIRECT (one chunk: acc is the output), atomics into acc otherwise.
+template <bool LAZY, bool DIRECT, bool PRE>
+__device__ __forceinline__ void chacha_tile(const uint32_t* __restrict__ seeds, uint32_t w, uint64_t s0, uint64_t s1,
+                                            uint64_t x, uint64_t D, unsigned long long* __restrict__ acc,
+                                            const Mod64& M, uint64_t zone, uint64_t r64, const RejectLog& log,
+                                            const ChachaPre* __restrict__ pre, unsigned long long* st) {
     const uint32_t tid = threadIdx.x;
-    const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + tid;
+    const uint64_t blk = x * 256 + tid;
     const uint64_t n_blk = (D + 7) / 8;
     const bool live = blk < n_blk;
-    const uint64_t s0 = (uint64_t)blockIdx.y * seeds_per_chunk;
     // the seed loop is uniform (lanes past D run it on draws they never keep), so each seed's key and
     // round-1 columns 1-3 are scalar work; a 256-block group never straddles 2^32, so the counter's high
     // word is uniform too
-    const uint64_t s1 = s0 + seeds_per_chunk < n_seeds ? s0 + seeds_per_chunk : n_seeds;
-    const uint32_t ctr_hi = (uint32_t)(((uint64_t)blockIdx.x * blockDim.x) >> 32);
+    const uint32_t ctr_hi = (uint32_t)((x * 256) >> 32);
     const uint32_t nw = w < 8 ? w : 8;
     const uint64_t m = M.m;
     const uint32_t nvalid = !live ? 0u : (D - blk * 8 < 8 ? (uint32_t)(D - blk * 8) : 8u);   // pairs inside D
@@ -132,50 +165,70 @@ __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __r
     uint32_t hi[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) { a[q] = 0; hi[q] = 0; }
-    for (uint64_t s = s0; s < s1; ++s) {
+    // one block's draws (seed S, words O): the rejection screen, then the running sums
+#define SDA_CHACHA_TAKE(S, O)                                                                                  \
+    do {                                                                                                       \
+        /* rejections (< 2^-28 per draw): one max over the 8 high words screens the block */                   \
+        const uint32_t hmax = max(max(max(O[0], O[2]), max(O[4], O[6])), max(max(O[8], O[10]), max(O[12], O[14]))); \
+        if (hmax >= zone_hi) {                                                                                 \
+            _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                                    \
+                const uint64_t v = ((uint64_t)O[2 * q] << 32) | O[2 * q + 1];                                  \
+                if ((uint32_t)q < nvalid && v >= zone) { /* rejected: log it */                               \
+                    const unsigned long long slot = atomicAdd(log.count, 1ull);                                \
+                    if (slot < log.cap) { log.seed_of[slot] = (uint32_t)(S); log.pair_of[slot] = blk * 8 + q; } \
+                }                                                                                              \
+            }                                                                                                  \
+        }                                                                                                      \
+        /* pairs past D are summed too and never stored (only the last block of the grid has any) */           \
+        _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                                        \
+            const uint64_t v = ((uint64_t)O[2 * q] << 32) | O[2 * q + 1]; /* high word first */                \
+            if constexpr (LAZY) {                                                                              \
+                const uint64_t y = a[q] + v;                                                                   \
+                hi[q] += y < v ? 1u : 0u;                                                                      \
+                a[q] = y;                                                                                      \
+            } else {                                                                                           \
+                const uint64_t y = a[q] + umod64(v, M);                                                        \
+                a[q] = y >= m ? y - m : y;                                                                     \
+            }                                                                                                  \
+        }                                                                                                      \
+    } while (0)
+    uint64_t s = s0;
+    if constexpr (SDA_CHACHA_PAIR) {             // two seeds per step, their rounds interleaved
+        for (; s + 1 < s1; s += 2) {
+            uint32_t ka[8], kb[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                ka[q] = (uint32_t)q < nw ? seeds[s * w + q] : 0u;          // uniform: scalar loads
+                kb[q] = (uint32_t)q < nw ? seeds[(s + 1) * w + q] : 0u;
+            }
+            uint32_t o[16], u[16];
+            chacha_block_pre_x2(PRE ? pre[s] : chacha_pre(ka, ctr_hi), ka, PRE ? pre[s + 1] : chacha_pre(kb, ctr_hi),
+                                kb, blk, o, u);
+            SDA_CHACHA_TAKE(s, o);
+            SDA_CHACHA_TAKE(s + 1, u);
+        }
+    }
+    for (; s < s1; ++s) {
         uint32_t key[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) key[q] = (uint32_t)q < nw ? seeds[s * w + q] : 0u;   // uniform: scalar loads
         uint32_t o[16];
         chacha_block_pre(PRE ? pre[s] : chacha_pre(key, ctr_hi), key, blk, o);
-        // rejections (< 2^-28 per draw): one max over the 8 high words screens the block
-        const uint32_t hmax = max(max(max(o[0], o[2]), max(o[4], o[6])), max(max(o[8], o[10]), max(o[12], o[14])));
-        if (hmax >= zone_hi) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint64_t v = ((uint64_t)o[2 * q] << 32) | o[2 * q + 1];
-                if ((uint32_t)q < nvalid && v >= zone) {                    // rejected: log it
-                    const unsigned long long slot = atomicAdd(log.count, 1ull);
-                    if (slot < log.cap) { log.seed_of[slot] = (uint32_t)s; log.pair_of[slot] = blk * 8 + q; }
-                }
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const uint64_t v = ((uint64_t)o[2 * q] << 32) | o[2 * q + 1];    // high word first
-            // pairs past D are summed too and never stored (only the last block of the grid has any)
-            if constexpr (LAZY) {
-                const uint64_t x = a[q] + v;
-                hi[q] += x < v ? 1u : 0u;
-                a[q] = x;
-            } else {
-                uint64_t x = a[q] + umod64(v, M);
-                a[q] = x >= m ? x - m : x;
-            }
-        }
+        SDA_CHACHA_TAKE(s, o);
     }
+#undef SDA_CHACHA_TAKE
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         uint64_t r = a[q];
         if constexpr (LAZY) {       // (hi 2^64 + lo) mod m, m <= 2^32: hi mod m < m, r64 = 2^64 mod m
             const uint64_t t = umod64((uint64_t)hi[q], M) * r64;          // < m^2 <= 2^64
-            const uint64_t x = umod64(t, M) + umod64(r, M);               // < 2m
-            r = x >= m ? x - m : x;
+            const uint64_t y = umod64(t, M) + umod64(r, M);               // < 2m
+            r = y >= m ? y - m : y;
         }
         st[tid * kChachaPad + q] = r;
     }
     __syncthreads();
-    const uint64_t e0 = (uint64_t)blockIdx.x * 2048;
+    const uint64_t e0 = x * 2048;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const uint32_t idx = j * 256 + tid;
@@ -185,6 +238,50 @@ __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __r
             if constexpr (DIRECT) acc[e] = r;
             else atomicAdd(&acc[e], r);
         }
+    }
+}
+
+// acc[i] += sum over seeds in this y-chunk of draw_i  (un-shifted), canonical per chunk.
+// Every draw is >= 0, so the reference's running `(r + draw) % m` equals (sum of draws) mod m.
+// LAZY (m <= 2^32): the raw 64-bit words v are summed into 96-bit accumulators (3 adds per draw)
+// and reduced once per chunk -- (sum of v) mod m == sum of (v mod m) mod m; otherwise each draw
+// is reduced with the 64-bit Barrett `%`.
+// PRE: round 1's uniform columns of every seed come precomputed from `pre` (chacha_pre_kernel, counter
+// high word 0: the grid then holds < 2^32 blocks); otherwise the kernel computes them per seed.
+template <bool LAZY, bool DIRECT, bool PRE = false>
+__global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __restrict__ seeds, uint32_t w, uint64_t n_seeds,
+                           uint64_t seeds_per_chunk, uint64_t D, unsigned long long* __restrict__ acc, Mod64 M,
+                           uint64_t zone, uint64_t r64, RejectLog log, const ChachaPre* __restrict__ pre = nullptr) {
+    __shared__ unsigned long long st[256 * kChachaPad];
+    const uint64_t s0 = (uint64_t)blockIdx.y * seeds_per_chunk;
+    const uint64_t s1 = s0 + seeds_per_chunk < n_seeds ? s0 + seeds_per_chunk : n_seeds;
+    chacha_tile<LAZY, DIRECT, PRE>(seeds, w, s0, s1, blockIdx.x, D, acc, M, zone, r64, log, pre, st);
+}
+
+// Stream-K form of the same combine: the (tile, seed) units, tile-major, split evenly over exactly one
+// round of resident workgroups (workgroup g takes units [g q + min(g, r), ..) -- q or q + 1 of them),
+// each walking its range as runs of consecutive seeds of one tile and adding every run's partials into
+// acc with atomics.  The chunked grid above rounds the work to whole (tile, chunk) workgroups: at the
+// bench shape (489 tiles x 256 seeds, 1,792 resident workgroups) it launched 1,956 of them, a second
+// round 9 % full behind the first.  Here every workgroup ends within one unit of the others.
+template <bool LAZY, bool PRE>
+__global__ __launch_bounds__(256) void chacha_combine_sk_kernel(const uint32_t* __restrict__ seeds, uint32_t w,
+                                                                uint64_t n_seeds, uint64_t q, uint64_t r, uint64_t D,
+                                                                unsigned long long* __restrict__ acc, Mod64 M,
+                                                                uint64_t zone, uint64_t r64, RejectLog log,
+                                                                const ChachaPre* __restrict__ pre) {
+    __shared__ unsigned long long st[256 * kChachaPad];
+    const uint64_t g = blockIdx.x;
+    const uint64_t u = g * q + (g < r ? g : r);
+    uint64_t left = q + (g < r ? 1 : 0);              // units still to do
+    uint64_t x = u / n_seeds, s0 = u - x * n_seeds;   // the first run's tile and seed (one division)
+    while (left) {
+        const uint64_t s1 = n_seeds - s0 < left ? n_seeds : s0 + left;
+        chacha_tile<LAZY, false, PRE>(seeds, w, s0, s1, x, D, acc, M, zone, r64, log, pre, st);
+        __syncthreads();                          // st is rewritten by the next run
+        left -= s1 - s0;
+        ++x;
+        s0 = 0;
     }
 }
 
@@ -503,6 +600,30 @@ hipError_t launch_chacha_stream(int64_t modulus, uint64_t D, const uint32_t* see
     return expand_streams(modulus, D, seed, w, 0, 1, mask, static_cast<char*>(work), s);
 }
 
+// Workgroups of 256 lanes of `kernel` resident at once on the current device: one full round of the
+// grid.  Cached per (device, which) -- a process may drive devices of different sizes; a racing first
+// call computes the same value twice, and the relaxed atomics make that benign.
+static int resident_wgs(int which, const void* kernel) {
+    static std::atomic<int> cache[64][4];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int cap = (dev >= 0 && dev < 64) ? cache[dev][which].load(std::memory_order_relaxed) : 0;
+    if (cap) return cap;
+    int cus = 0, per_cu = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0);
+    // the API can be one block per CU high at 81-96 SGPRs (MI355X_MICROARCH.md): also bound it by the
+    // VGPR allocation (8-register granule, 512 per SIMD lane, 4 waves per block of 256)
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, kernel) == hipSuccess && fa.numRegs > 0) {
+        const int by_vgpr = 512 / (((fa.numRegs + 7) / 8) * 8);
+        if (by_vgpr < per_cu) per_cu = by_vgpr;
+    }
+    cap = (cus > 0 && per_cu > 0) ? cus * per_cu : 2048;
+    if (dev >= 0 && dev < 64) cache[dev][which].store(cap, std::memory_order_relaxed);
+    return cap;
+}
+
 // ---- fast path (counter mode + rejection log) ----
 // Split in two so a pipeline can keep queueing work behind the combine: chacha_fast_enqueue launches it
 // (canonical results land in `out`) and copies the rejection count to `count_host` (pinned); once the
@@ -528,37 +649,31 @@ static hipError_t chacha_fast_enqueue(int64_t modulus, uint64_t D, const uint32_
     // Seeds split over grid.y chunks until the grid holds one full round of resident workgroups (the
     // kernel is VALU-bound: more chunks only add atomic merges -- A/B in profiles/r02/ab_chacha.txt).
     // The u64 accumulators receive one canonical partial (< m) per chunk (headroom).
-    // cached per device (a process may drive devices of different sizes); a racing first call computes
-    // the same value twice, and the relaxed atomic makes that benign
-    static std::atomic<int> cap_cache[64];
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    int cap_wgs = (dev >= 0 && dev < 64) ? cap_cache[dev].load(std::memory_order_relaxed) : 0;
-    if (cap_wgs == 0) {
-        int cus = 0, per_cu = 0;
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chacha_combine_kernel<true, false, true>, 256, 0);
-        // the API can be one block per CU high at 81-96 SGPRs (MI355X_MICROARCH.md): also bound it by
-        // the VGPR allocation (8-register granule, 512 per SIMD lane, 4 waves per block of 256)
-        hipFuncAttributes fa{};
-        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(chacha_combine_kernel<true, false, true>)) == hipSuccess &&
-            fa.numRegs > 0) {
-            const int by_vgpr = 512 / (((fa.numRegs + 7) / 8) * 8);
-            if (by_vgpr < per_cu) per_cu = by_vgpr;
-        }
-        cap_wgs = (cus > 0 && per_cu > 0) ? cus * per_cu : 2048;
-        if (dev >= 0 && dev < 64) cap_cache[dev].store(cap_wgs, std::memory_order_relaxed);
-    }
+    const int cap_wgs = lazy ? resident_wgs(0, reinterpret_cast<const void*>(chacha_combine_kernel<true, false, true>))
+                             : resident_wgs(1, reinterpret_cast<const void*>(chacha_combine_kernel<false, false, true>));
+    const int cap_sk = lazy ? resident_wgs(2, reinterpret_cast<const void*>(chacha_combine_sk_kernel<true, true>))
+                            : resident_wgs(3, reinterpret_cast<const void*>(chacha_combine_sk_kernel<false, true>));
     uint64_t max_c = n_seeds ? n_seeds : 1;
     if (max_c > 65535) max_c = 65535;
     if (M.m > 1 && max_c > UINT64_MAX / (M.m - 1)) max_c = UINT64_MAX / (M.m - 1);
     uint64_t chunks = ((uint64_t)cap_wgs + gx - 1) / gx;
     if (chunks > max_c) chunks = max_c;
-    if (const char* ce = getenv("SDA_CHACHA_CHUNKS")) {          // A/B knob
+    const char* ce = getenv("SDA_CHACHA_CHUNKS");                 // A/B knob: the chunked grid, c chunks
+    if (ce) {
         const uint64_t c = strtoull(ce, nullptr, 10);
         if (c >= 1 && c <= max_c) chunks = c;
     }
     if (secrets) chunks = 1;                     // one stream: its own grid, no accumulator
+    // Stream-K (chacha_combine_sk_kernel) when the chunked grid leaves a partial last round of workgroups
+    // (< 95 % of its rounds' slots busy) and every tile's runs fit the u64 accumulator's headroom.
+    const uint64_t units = gx * n_seeds, G = units < (uint64_t)cap_sk ? units : (uint64_t)cap_sk;
+    const uint64_t chunk_wgs = gx * chunks, rounds = (chunk_wgs + cap_wgs - 1) / cap_wgs;
+    const uint64_t per_wg = G ? units / G : 0;
+    const uint64_t runs_per_tile = per_wg ? (n_seeds + per_wg - 1) / per_wg + 1 : UINT64_MAX;
+    const char* ske = getenv("SDA_CHACHA_SK");                    // A/B knob: "0" = the chunked grid
+    const bool sk = !secrets && !ce && !(ske && ske[0] == '0') && n_seeds && G && runs_per_tile <= max_c &&
+                    (double)chunk_wgs < 0.95 * (double)(rounds * (uint64_t)cap_wgs);
+    if (sk) chunks = 2;                          // not direct: acc is zeroed, merged and reduced below
     const uint64_t per = n_seeds ? (n_seeds + chunks - 1) / chunks : 0;
     const bool direct = chunks == 1;             // results stored straight into `out`
     unsigned long long* dst = direct ? reinterpret_cast<unsigned long long*>(out) : acc;
@@ -585,7 +700,21 @@ static hipError_t chacha_fast_enqueue(int64_t modulus, uint64_t D, const uint32_
                                per, D, dst, M, zone, r64, log, (const ChachaPre*)nullptr);                    \
     } while (0)
     const bool small_m = mm <= (1ull << 62);
-    if (secrets)
+    if (sk) {
+        const uint64_t q = units / G, r = units % G;
+        if (lazy && use_pre)
+            hipLaunchKernelGGL((chacha_combine_sk_kernel<true, true>), dim3((unsigned)G), dim3(256), 0, s, seeds_dev, w,
+                               n_seeds, q, r, D, acc, M, zone, r64, log, (const ChachaPre*)pre);
+        else if (lazy)
+            hipLaunchKernelGGL((chacha_combine_sk_kernel<true, false>), dim3((unsigned)G), dim3(256), 0, s, seeds_dev, w,
+                               n_seeds, q, r, D, acc, M, zone, r64, log, (const ChachaPre*)nullptr);
+        else if (use_pre)
+            hipLaunchKernelGGL((chacha_combine_sk_kernel<false, true>), dim3((unsigned)G), dim3(256), 0, s, seeds_dev, w,
+                               n_seeds, q, r, D, acc, M, zone, r64, log, (const ChachaPre*)pre);
+        else
+            hipLaunchKernelGGL((chacha_combine_sk_kernel<false, false>), dim3((unsigned)G), dim3(256), 0, s, seeds_dev, w,
+                               n_seeds, q, r, D, acc, M, zone, r64, log, (const ChachaPre*)nullptr);
+    } else if (secrets)
         hipLaunchKernelGGL(chacha_mask_add_kernel, dim3((unsigned)gx), dim3(256), 0, s, seeds_dev, w, D, dst, M, zone,
                            log, secrets, small_m);
     else if (lazy && direct) SDA_CHACHA_LAUNCH(true, true);

@@ -15,7 +15,6 @@
 #include <stdlib.h>
 
 #include "kernels.h"
-#include "xcd.h"
 
 namespace sda {
 
@@ -43,11 +42,10 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict_
                                                             uint64_t n, uint64_t n_lanes,
                                                             uint64_t stride,
                                                             int64_t* __restrict__ out, Mod64 M,
-                                                            int64_t* __restrict__ flags = nullptr, int xcd = 0) {
+                                                            int64_t* __restrict__ flags = nullptr) {
     typedef typename vec_t<T, VEC>::type V;
-    // xcd: each XCD walks one contiguous eighth of the column strips (xcd.h)
-    const uint64_t blk = xcd ? xcd_chunk(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint64_t lane = blk * blockDim.x + threadIdx.x;
+    // (natural workgroup order: the XCD-chunked order of xcd.h measured neutral here, profiles/r04b)
+    const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= n_lanes) return;
     const V* p = reinterpret_cast<const V*>(in + lane * VEC);
     const uint64_t vstride = stride / VEC;     // stride in units of V (host guarantees divisibility)
@@ -99,16 +97,12 @@ hipError_t launch_vec(const T* in, uint64_t n, uint64_t dim, uint64_t stride, in
                       const Mod64& M, bool small_m, hipStream_t s, int64_t* flags = nullptr) {
     const uint64_t n_lanes = dim / VEC;
     const uint64_t blocks = (n_lanes + 255) / 256;
-    static const int xcd = [] {                      // A/B knob: SDA_XCD_COMBINE=0 (natural order)
-        const char* e = getenv("SDA_XCD_COMBINE");
-        return e && e[0] == '0' ? 0 : 1;
-    }();
     if (small_m)
         hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, true, ACC, FLAG>), dim3((unsigned)blocks), dim3(256),
-                           0, s, in, n, n_lanes, stride, out, M, flags, xcd);
+                           0, s, in, n, n_lanes, stride, out, M, flags);
     else
         hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, false, ACC, FLAG>), dim3((unsigned)blocks), dim3(256),
-                           0, s, in, n, n_lanes, stride, out, M, flags, xcd);
+                           0, s, in, n, n_lanes, stride, out, M, flags);
     return hipGetLastError();
 }
 

@@ -41,6 +41,7 @@ struct sda_engine {
     // than the previous one first waits (on the device) for the work queued on that stream.
     hipStream_t last_stream = nullptr;
     hipEvent_t order_ev = nullptr;
+    bool order_ok = true;         // order_ev was recorded when the last call ended (else: host sync)
     unsigned long long* rej_host = nullptr;   // pinned: the ChaCha rejection count of a pipeline's mask
 };
 
@@ -56,13 +57,26 @@ thread_local hipStream_t t_call_s = nullptr;
 
 void end_call() {
     if (t_call_h) {
-        (void)hipEventRecord(t_call_h->order_ev, t_call_s);
+        t_call_h->order_ok = hipEventRecord(t_call_h->order_ev, t_call_s) == hipSuccess;
         t_call_h = nullptr;
     }
 }
 
+// Every extern "C" entry point opens a CallScope (SDA_ENTRY) as its first statement; the outermost scope
+// ends the call's ordering scope (end_call) on every return path, after everything the call queued.
+// Internal helpers -- and entry points called from entry points -- may return ok()/fail() freely.
+thread_local int t_depth = 0;
+struct CallScope {
+    CallScope() { ++t_depth; }
+    ~CallScope() {
+        if (--t_depth == 0) end_call();
+    }
+    CallScope(const CallScope&) = delete;
+    CallScope& operator=(const CallScope&) = delete;
+};
+#define SDA_ENTRY CallScope sda_call_scope_
+
 sda_status fail(sda_status st, const char* fmt, ...) {
-    end_call();
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -73,7 +87,6 @@ sda_status fail(sda_status st, const char* fmt, ...) {
 }
 
 sda_status ok() {
-    end_call();
     g_last_error.clear();
     return SDA_OK;
 }
@@ -106,8 +119,9 @@ sda_status ensure(void** buf, size_t* have, size_t need) {
 hipStream_t pick(sda_engine* h, void* stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (s != h->last_stream) {
-        if (hipStreamWaitEvent(s, h->order_ev, 0) != hipSuccess)
-            (void)hipEventSynchronize(h->order_ev);          // same ordering, from the host
+        // a failed record leaves a stale event: order from the host instead (the previous stream may be
+        // gone, so the whole device)
+        if (!h->order_ok || hipStreamWaitEvent(s, h->order_ev, 0) != hipSuccess) (void)hipDeviceSynchronize();
         h->last_stream = s;
     }
     t_call_h = h;
@@ -267,6 +281,7 @@ int sda_abi_version(void) { return SDA_ENGINE_ABI_VERSION; }
 const char* sda_last_error_message(void) { return g_last_error.c_str(); }
 
 const char* sda_status_string(int st) {
+    SDA_ENTRY;
     switch (st) {
         case SDA_OK: return "ok";
         case SDA_ERR_BATCH_INPUT_WRONG_LENGTH: return "Batch input wrong length";
@@ -285,6 +300,7 @@ const char* sda_status_string(int st) {
 }
 
 sda_status sda_engine_create(int device_ordinal, sda_engine** out) {
+    SDA_ENTRY;
     if (!out) return fail(SDA_ERR_INVALID_ARGUMENT, "out is NULL");
     *out = nullptr;
     int n = 0;
@@ -309,6 +325,7 @@ sda_status sda_engine_create(int device_ordinal, sda_engine** out) {
 }
 
 void sda_engine_destroy(sda_engine* h) {
+    SDA_ENTRY;
     if (!h) return;
     if (t_call_h == h) t_call_h = nullptr;
     (void)hipSetDevice(h->device);
@@ -329,6 +346,7 @@ void sda_engine_destroy(sda_engine* h) {
 }
 
 sda_status sda_engine_synchronize(sda_engine* h) {
+    SDA_ENTRY;
     if (!h) return fail(SDA_ERR_INVALID_ARGUMENT, "engine handle is NULL");
     HIP_TRY(hipDeviceSynchronize());
     return ok();
@@ -336,16 +354,20 @@ sda_status sda_engine_synchronize(sda_engine* h) {
 
 // ---------------- protocol/src/crypto.rs:117-155 ----------------
 uint64_t sda_scheme_input_size(const sda_sharing_scheme* s) {
+    SDA_ENTRY;
     return s->kind == SDA_SHARING_ADDITIVE ? 1 : s->secret_count;
 }
 uint64_t sda_scheme_output_size(const sda_sharing_scheme* s) { return s->share_count; }
 uint64_t sda_scheme_privacy_threshold(const sda_sharing_scheme* s) {
+    SDA_ENTRY;
     return s->kind == SDA_SHARING_ADDITIVE ? s->share_count - 1 : s->privacy_threshold;
 }
 uint64_t sda_scheme_reconstruction_threshold(const sda_sharing_scheme* s) {
+    SDA_ENTRY;
     return s->kind == SDA_SHARING_ADDITIVE ? s->share_count : s->privacy_threshold + s->secret_count;
 }
 uint64_t sda_share_length(const sda_sharing_scheme* s, uint64_t dimension) {
+    SDA_ENTRY;
     const uint64_t k = sda_scheme_input_size(s);
     return k ? (dimension + k - 1) / k : 0;
 }
@@ -353,6 +375,7 @@ uint64_t sda_share_length(const sda_sharing_scheme* s, uint64_t dimension) {
 // ---------------- ShareGenerator::generate ----------------
 sda_status sda_share_generate(sda_engine* h, const sda_sharing_scheme* s, const int64_t* secrets, uint64_t D,
                               const int64_t* draws, uint64_t n_draws, int64_t* out, uint64_t out_cap) {
+    SDA_ENTRY;
     if (!h || !s) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL handle or scheme");
     if ((D && !secrets) || (n_draws && !draws)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL input buffer");
     HIP_TRY(hipSetDevice(h->device));
@@ -410,6 +433,9 @@ static sda_status combine_rows(sda_engine* h, int64_t modulus, const int64_t* co
     const uint64_t dim = n_rows ? lens[0] : 0;              // combiner.rs:17
     *out_len = 0;
     int64_t m;
+    // combiner.rs:20-25 / additive.rs:62-67: row 0 (of length dim) is folded -- `%= 0` panics there --
+    // before row 1's length is checked
+    if (dim && modulus == 0) return modulus_abs(modulus, &m);
     for (uint64_t i = 0; i < n_rows; ++i)
         if (lens[i] != dim) return fail(dim_err, "%s (row %llu has %llu elements, expected %llu)", dim_msg,
                                         (unsigned long long)i, (unsigned long long)lens[i],
@@ -437,6 +463,7 @@ static sda_status combine_rows(sda_engine* h, int64_t modulus, const int64_t* co
 sda_status sda_share_combine(sda_engine* h, const sda_sharing_scheme* s, const int64_t* const* rows,
                              const uint64_t* lens, uint64_t n_rows, int64_t* out, uint64_t out_cap,
                              uint64_t* out_len) {
+    SDA_ENTRY;
     if (!s) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL scheme");
     // sharing/mod.rs:61-69: Additive -> modulus, PackedShamir -> prime_modulus (same field here)
     return combine_rows(h, s->modulus, rows, lens, n_rows, out, out_cap, out_len, SDA_ERR_WRONG_DIMENSION,
@@ -447,6 +474,7 @@ sda_status sda_share_combine(sda_engine* h, const sda_sharing_scheme* s, const i
 sda_status sda_secret_reconstruct(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,
                                   const uint64_t* indices, const int64_t* const* rows, const uint64_t* lens,
                                   uint64_t n_rows, int64_t* out, uint64_t out_cap, uint64_t* out_len) {
+    SDA_ENTRY;
     if (!h || !s || !out_len) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     if (s->kind == SDA_SHARING_ADDITIVE) {
         // additive.rs:56-72: dimension = first row's length; indices are ignored
@@ -494,6 +522,7 @@ sda_status sda_secret_reconstruct(sda_engine* h, const sda_sharing_scheme* s, ui
 sda_status sda_secret_mask(sda_engine* h, const sda_masking_scheme* s, const int64_t* secrets, uint64_t D,
                            const uint32_t* seed, uint64_t seed_words, const int64_t* full_masks, int64_t* mask_out,
                            uint64_t mask_cap, uint64_t* mask_len, int64_t* masked_out) {
+    SDA_ENTRY;
     if (!h || !s || !mask_len || (D && (!secrets || !masked_out)))
         return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     HIP_TRY(hipSetDevice(h->device));
@@ -547,6 +576,7 @@ sda_status sda_secret_mask(sda_engine* h, const sda_masking_scheme* s, const int
 sda_status sda_mask_combine(sda_engine* h, const sda_masking_scheme* s, const int64_t* const* rows,
                             const uint64_t* lens, uint64_t n_rows, int64_t* out, uint64_t out_cap,
                             uint64_t* out_len) {
+    SDA_ENTRY;
     if (!h || !s || !out_len || (n_rows && (!rows || !lens))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     *out_len = 0;
     if (s->kind == SDA_MASKING_NONE) {                      // none.rs:22-25
@@ -589,6 +619,7 @@ sda_status sda_mask_combine(sda_engine* h, const sda_masking_scheme* s, const in
 sda_status sda_secret_unmask(sda_engine* h, const sda_masking_scheme* s, const int64_t* mask, uint64_t mask_len,
                              const int64_t* masked, uint64_t masked_len, int64_t* out, uint64_t out_cap,
                              uint64_t* out_len) {
+    SDA_ENTRY;
     if (!h || !s || !out_len || (masked_len && (!masked || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     *out_len = 0;
     if (out_cap < masked_len) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
@@ -620,6 +651,7 @@ sda_status sda_secret_unmask(sda_engine* h, const sda_masking_scheme* s, const i
 }
 
 sda_status sda_recipient_positive(sda_engine* h, int64_t modulus, const int64_t* values, uint64_t n, int64_t* out) {
+    SDA_ENTRY;
     if (!h || (n && (!values || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     if (n == 0) return ok();
     HIP_TRY(hipSetDevice(h->device));
@@ -636,6 +668,7 @@ sda_status sda_recipient_positive(sda_engine* h, int64_t modulus, const int64_t*
 // ---------------- device-resident entry points ----------------
 sda_status sda_combine_dev(sda_engine* h, int64_t modulus, const int64_t* shares, uint64_t n, uint64_t dim,
                            uint64_t row_stride, int64_t* out, void* stream) {
+    SDA_ENTRY;
     if (!h || (dim && (!out || (n && !shares)))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     if (n > 1 && row_stride < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "row_stride < dim");
     int64_t m;
@@ -647,6 +680,7 @@ sda_status sda_combine_dev(sda_engine* h, int64_t modulus, const int64_t* shares
 
 sda_status sda_combine_accumulate_dev(sda_engine* h, int64_t modulus, const int64_t* shares, uint64_t n,
                                       uint64_t dim, uint64_t row_stride, int64_t* inout, void* stream) {
+    SDA_ENTRY;
     if (!h || (dim && (!inout || (n && !shares)))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     if (n > 1 && row_stride < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "row_stride < dim");
     int64_t m;
@@ -659,6 +693,7 @@ sda_status sda_combine_accumulate_dev(sda_engine* h, int64_t modulus, const int6
 
 sda_status sda_combine_finalize_dev(sda_engine* h, int64_t modulus, const int64_t* sums, uint64_t dim, int64_t* out,
                                     void* stream) {
+    SDA_ENTRY;
     if (!h || (dim && (!sums || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     int64_t m;
     if (sda_status st = modulus_abs(modulus, &m)) return st;
@@ -669,6 +704,7 @@ sda_status sda_combine_finalize_dev(sda_engine* h, int64_t modulus, const int64_
 
 sda_status sda_combine_split_dev(sda_engine* h, int64_t modulus, const int64_t* shares, uint64_t n, uint64_t dim,
                                  uint64_t row_stride, int64_t* inout, int64_t* flags, void* stream) {
+    SDA_ENTRY;
     if (!h || (dim && (!inout || !flags || (n && !shares)))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     if (n > 1 && row_stride < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "row_stride < dim");
     int64_t m;
@@ -681,6 +717,7 @@ sda_status sda_combine_split_dev(sda_engine* h, int64_t modulus, const int64_t* 
 sda_status sda_combine_split_prefix_dev(sda_engine* h, int64_t modulus, const int64_t* gathered, uint64_t world,
                                         uint64_t rank, uint64_t dim, int64_t* c_in, int64_t* total, int32_t* code,
                                         void* stream) {
+    SDA_ENTRY;
     if (!h || (dim && (!gathered || !c_in || !total || !code))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     if (rank >= world || world > (1u << 29)) return fail(SDA_ERR_INVALID_ARGUMENT, "rank %llu of world %llu",
                                                          (unsigned long long)rank, (unsigned long long)world);
@@ -696,6 +733,7 @@ sda_status sda_combine_split_prefix_dev(sda_engine* h, int64_t modulus, const in
 sda_status sda_combine_split_replay_dev(sda_engine* h, int64_t modulus, const int64_t* shares, uint64_t n,
                                         uint64_t dim, uint64_t row_stride, uint64_t rank, int64_t* state,
                                         int32_t* code, void* stream) {
+    SDA_ENTRY;
     if (!h || (dim && (!state || !code || (n && !shares)))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     if (n > 1 && row_stride < dim) return fail(SDA_ERR_INVALID_ARGUMENT, "row_stride < dim");
     if (rank > (1u << 29)) return fail(SDA_ERR_INVALID_ARGUMENT, "rank %llu too large", (unsigned long long)rank);
@@ -709,6 +747,7 @@ sda_status sda_combine_split_replay_dev(sda_engine* h, int64_t modulus, const in
 
 sda_status sda_combine_split_resolve_dev(sda_engine* h, int64_t modulus, const int64_t* total, const int32_t* code,
                                          uint64_t dim, int64_t* out, void* stream) {
+    SDA_ENTRY;
     if (!h || (dim && (!total || !code || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     int64_t m;
     if (sda_status st = modulus_abs(modulus, &m)) return st;
@@ -720,6 +759,7 @@ sda_status sda_combine_split_resolve_dev(sda_engine* h, int64_t modulus, const i
 sda_status sda_packed_generate_dev(sda_engine* h, const sda_sharing_scheme* s, const int64_t* secrets,
                                    uint64_t dimension, uint64_t n_vectors, const int64_t* draws, int64_t* out,
                                    void* stream) {
+    SDA_ENTRY;
     if (!h || !s || s->kind != SDA_SHARING_PACKED_SHAMIR) return fail(SDA_ERR_INVALID_ARGUMENT, "need a PackedShamir scheme");
     if (sda_status st = check_packed(s)) return st;
     if (n_vectors > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 vectors per launch");
@@ -735,6 +775,7 @@ sda_status sda_packed_generate_dev(sda_engine* h, const sda_sharing_scheme* s, c
 sda_status sda_packed_generate_mode_dev(sda_engine* h, const sda_sharing_scheme* s, const int64_t* secrets,
                                         uint64_t dimension, uint64_t n_vectors, const int64_t* draws, int64_t* out,
                                         int32_t mode, void* stream) {
+    SDA_ENTRY;
     if (!h || !s || s->kind != SDA_SHARING_PACKED_SHAMIR) return fail(SDA_ERR_INVALID_ARGUMENT, "need a PackedShamir scheme");
     if (mode != SDA_REVEAL_EXACT && mode != SDA_REVEAL_CANONICAL) return fail(SDA_ERR_INVALID_ARGUMENT, "bad mode");
     if (sda_status st = check_packed(s)) return st;
@@ -751,6 +792,7 @@ sda_status sda_packed_generate_mode_dev(sda_engine* h, const sda_sharing_scheme*
 sda_status sda_packed_reconstruct_dev(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,
                                       const uint64_t* indices, uint64_t n_idx, uint64_t n_vectors,
                                       const int64_t* shares, int64_t* out, int32_t mode, void* stream) {
+    SDA_ENTRY;
     if (!h || !s || s->kind != SDA_SHARING_PACKED_SHAMIR) return fail(SDA_ERR_INVALID_ARGUMENT, "need a PackedShamir scheme");
     if (sda_status st = check_packed(s)) return st;
     if (mode != SDA_REVEAL_EXACT && mode != SDA_REVEAL_CANONICAL) return fail(SDA_ERR_INVALID_ARGUMENT, "bad mode");
@@ -775,6 +817,7 @@ sda_status sda_packed_reconstruct_dev(sda_engine* h, const sda_sharing_scheme* s
 
 sda_status sda_additive_generate_dev(sda_engine* h, int64_t modulus, uint64_t share_count, const int64_t* secrets,
                                      uint64_t dimension, const int64_t* draws, int64_t* out, void* stream) {
+    SDA_ENTRY;
     if (!h) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL handle");
     if (share_count == 0) return fail(SDA_ERR_PRECONDITION, "share_count - 1 underflows (additive.rs:42)");
     if (modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
@@ -785,6 +828,7 @@ sda_status sda_additive_generate_dev(sda_engine* h, int64_t modulus, uint64_t sh
 
 sda_status sda_chacha_mask_combine_dev(sda_engine* h, int64_t modulus, uint64_t dimension, const uint32_t* seeds,
                                        uint64_t w, uint64_t n_seeds, int64_t* out, void* stream) {
+    SDA_ENTRY;
     if (!h || (dimension && !out) || (n_seeds && w && !seeds)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     if (dimension && modulus <= 0) return fail(SDA_ERR_PRECONDITION, "Rng.gen_range called with low >= high");
     if (w == 0 || w > 8) return fail(SDA_ERR_INVALID_ARGUMENT, "seed width must be 1..8 words");
@@ -796,6 +840,7 @@ sda_status sda_chacha_mask_combine_dev(sda_engine* h, int64_t modulus, uint64_t 
 
 sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64_t cols, uint64_t seed, int64_t lo,
                               int64_t hi, void* stream) {
+    SDA_ENTRY;
     if (!h || (rows * cols && !dst)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     if (hi <= lo) return fail(SDA_ERR_INVALID_ARGUMENT, "need hi > lo");
     HIP_TRY(hipSetDevice(h->device));
@@ -863,12 +908,13 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
                                                         &flags, st));
         if (!(flags & 1u)) {
             const uint64_t dim = counts[0];
+            int64_t mm = 1;
+            if (dim && m == 0) return modulus_abs(m, &mm);     // blob 0 is folded first (combiner.rs:20-25)
             for (uint64_t i = 1; i < n_blobs; ++i)
                 if (counts[i] != dim)
                     return fail(SDA_ERR_WRONG_DIMENSION,
                                 "Wrong dimension (participation %llu decodes to %llu shares, expected %llu)",
                                 (unsigned long long)i, (unsigned long long)counts[i], (unsigned long long)dim);
-            int64_t mm = 1;
             if (dim) {
                 if (sda_status e = modulus_abs(m, &mm)) return e;
             }
@@ -882,11 +928,12 @@ sda_status decode_combine(sda_engine* h, int64_t m, const uint8_t* bytes, const 
                                    &long_elems))
         return e;
     const uint64_t dim = counts[0];
+    int64_t mm;
+    if (dim && m == 0) return modulus_abs(m, &mm);             // blob 0 is folded first (combiner.rs:20-25)
     for (uint64_t i = 1; i < n_blobs; ++i)
         if (counts[i] != dim)
             return fail(SDA_ERR_WRONG_DIMENSION, "Wrong dimension (participation %llu decodes to %llu shares, expected %llu)",
                         (unsigned long long)i, (unsigned long long)counts[i], (unsigned long long)dim);
-    int64_t mm;
     if (dim) {
         if (sda_status e = modulus_abs(m, &mm)) return e;
     }
@@ -944,6 +991,7 @@ extern "C" {
 
 sda_status sda_varint_encode(sda_engine* h, const int64_t* vals, uint64_t n, uint8_t* out, uint64_t out_cap,
                              uint64_t* out_len) {
+    SDA_ENTRY;
     if (!h || !out_len || (n && !vals)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     *out_len = 0;
     if (n == 0) return ok();
@@ -965,6 +1013,7 @@ sda_status sda_varint_encode(sda_engine* h, const int64_t* vals, uint64_t n, uin
 
 sda_status sda_varint_decode(sda_engine* h, const uint8_t* bytes, uint64_t n_bytes, int64_t* out, uint64_t out_cap,
                              uint64_t* out_len) {
+    SDA_ENTRY;
     if (!h || !out_len || (n_bytes && !bytes)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     *out_len = 0;
     HIP_TRY(hipSetDevice(h->device));
@@ -990,6 +1039,7 @@ sda_status sda_varint_decode(sda_engine* h, const uint8_t* bytes, uint64_t n_byt
 sda_status sda_clerk_decode_combine(sda_engine* h, const sda_sharing_scheme* s, const uint8_t* const* blobs,
                                     const uint64_t* blob_lens, uint64_t n_blobs, int64_t* out, uint64_t out_cap,
                                     uint64_t* out_len) {
+    SDA_ENTRY;
     if (!h || !s || !out_len || (n_blobs && (!blobs || !blob_lens))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     *out_len = 0;
     HIP_TRY(hipSetDevice(h->device));
@@ -1012,6 +1062,7 @@ sda_status sda_clerk_decode_combine(sda_engine* h, const sda_sharing_scheme* s, 
 
 sda_status sda_varint_decode_dev(sda_engine* h, const uint8_t* bytes, const uint64_t* blob_off, uint64_t n_blobs,
                                  int64_t* out, uint64_t out_stride, uint64_t* counts, void* stream) {
+    SDA_ENTRY;
     if (!h || !blob_off || !counts || (n_blobs && (!bytes || !out))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = pick(h, stream);
@@ -1039,6 +1090,7 @@ sda_status sda_varint_decode_dev(sda_engine* h, const uint8_t* bytes, const uint
 sda_status sda_clerk_decode_combine_dev(sda_engine* h, int64_t modulus, const uint8_t* bytes, const uint64_t* blob_off,
                                         uint64_t n_blobs, int64_t* out, uint64_t out_cap, uint64_t* out_len,
                                         void* stream) {
+    SDA_ENTRY;
     if (!h || !blob_off || !out_len || (n_blobs && !bytes)) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     HIP_TRY(hipSetDevice(h->device));
     if (sda_status e = decode_combine(h, modulus, bytes, blob_off, n_blobs, out, out_cap, out_len, pick(h, stream)))
@@ -1048,6 +1100,7 @@ sda_status sda_clerk_decode_combine_dev(sda_engine* h, int64_t modulus, const ui
 
 sda_status sda_varint_encode_dev(sda_engine* h, const int64_t* vals, uint64_t rows, uint64_t len, uint64_t stride,
                                  uint8_t* dst, uint64_t dst_cap, uint64_t* row_bytes, void* stream) {
+    SDA_ENTRY;
     if (!h || !row_bytes || (rows && len && (!vals || !dst))) return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     if (rows > 65535) return fail(SDA_ERR_UNSUPPORTED, "at most 65535 rows per call");
     if (stride < len) return fail(SDA_ERR_INVALID_ARGUMENT, "stride < len");
@@ -1065,6 +1118,7 @@ sda_status sda_varint_encode_dev(sda_engine* h, const int64_t* vals, uint64_t ro
 sda_status sda_snapshot_transpose_dev(sda_engine* h, const uint8_t* src, const uint64_t* part_off,
                                       uint64_t n_participations, uint64_t n_clerks, uint8_t* dst, uint64_t dst_cap,
                                       uint64_t* dst_len, uint64_t* clerk_base, uint64_t* clerk_off, void* stream) {
+    SDA_ENTRY;
     if (!h || !part_off || !dst_len || (n_clerks && (!clerk_base || !clerk_off)))
         return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     const uint64_t P = n_participations, n = n_clerks, nb = P * n;
@@ -1242,6 +1296,7 @@ sda_status sda_recipient_reveal_dev(sda_engine* h, const sda_masking_scheme* ms,
                                     const uint64_t* indices, const int64_t* shares, uint64_t n_idx,
                                     uint64_t share_len, int64_t output_modulus, int32_t mode, int64_t* out,
                                     uint64_t out_cap, uint64_t* out_len, void* stream) {
+    SDA_ENTRY;
     if (!h || !ms || !ss || !out_len || (n_idx && (!shares || !indices)) || (n_masks && mask_width && !mask_in))
         return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     HIP_TRY(hipSetDevice(h->device));
@@ -1256,6 +1311,7 @@ sda_status sda_recipient_reveal(sda_engine* h, const sda_masking_scheme* ms, con
                                 uint64_t dimension, const uint64_t* indices, const int64_t* const* share_rows,
                                 const uint64_t* share_lens, uint64_t n_idx, int64_t output_modulus, int32_t mode,
                                 int64_t* out, uint64_t out_cap, uint64_t* out_len) {
+    SDA_ENTRY;
     if (!h || !ms || !ss || !out_len || (n_masks && (!mask_rows || !mask_lens)) ||
         (n_idx && (!share_rows || !share_lens || !indices)))
         return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
@@ -1316,6 +1372,7 @@ sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms
                                      const int64_t* secrets, uint64_t dimension, const int64_t* draws,
                                      int32_t mode, int64_t* shares_out, uint8_t* payload, uint64_t payload_cap,
                                      uint64_t* payload_row_bytes, void* stream) {
+    SDA_ENTRY;
     if (!h || !ms || !ss || (dimension && (!secrets || !shares_out)) || (payload && !payload_row_bytes))
         return fail(SDA_ERR_INVALID_ARGUMENT, "NULL argument");
     HIP_TRY(hipSetDevice(h->device));

@@ -225,10 +225,14 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
 
     {
         const GenTables& T = *Tp;
-        // XCD-chunked tile order (xcd.h): each XCD streams one contiguous eighth of the [vector][tile] grid
-        const uint64_t lin = xcd ? xcd_linear_block() : blockIdx.x + (uint64_t)blockIdx.y * gridDim.x;
-        const uint32_t vec = (uint32_t)(lin / gridDim.x);
-        const uint64_t b0 = (lin % gridDim.x) * BS;
+        // XCD-chunked tile order (xcd.h): each XCD streams one contiguous eighth of the [vector][tile] grid.
+        // Only for the transforms up to L = 16 (the benchmarked sizes): the wide register kernels run at
+        // 1-2 waves with their registers full, and keep the natural order's code unchanged.
+        uint32_t tile = blockIdx.x, vec = blockIdx.y;
+        if constexpr (L <= 16) {
+            if (xcd) xcd_block_xy(&tile, &vec);
+        }
+        const uint64_t b0 = (uint64_t)tile * BS;
         const int64_t* sec = secrets + (uint64_t)vec * D;
 
         // ---- stage the tile's inputs through LDS with coalesced loads ----
@@ -484,7 +488,7 @@ static void gen_launch_mode(const PackedGenArgs& a, uint32_t k, uint32_t t, uint
     constexpr int BS = gen_block<L>();
     const dim3 grid((unsigned)((B + BS - 1) / BS), (unsigned)a.n_vectors);
     const bool wide = B % 2 == 0 && ((uintptr_t)a.out % 16) == 0;
-    const int xcd = a.xcd_order ? 1 : 0;
+    const int xcd = a.xcd_order && (uint64_t)grid.x * grid.y < (1ull << 32) ? 1 : 0;
     if (wide && !CANON && p >= kLazyTruncMinP && a.signbit)   // exact shares, sign-bit radix-2 half
         hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, false, true, true>), grid, dim3(BS), 0, s, a.secrets,
                            a.dimension, a.draws, a.out, k, t, B, T, log.count, xcd);

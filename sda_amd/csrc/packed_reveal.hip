@@ -229,11 +229,15 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
                                                                   unsigned int* __restrict__ log, int xcd) {
     extern __shared__ int64_t lds_o[];
     const uint32_t tid = threadIdx.x;
-    // XCD-chunked tile order (xcd.h)
-    const uint64_t lin = xcd ? xcd_linear_block() : blockIdx.x + (uint64_t)blockIdx.y * gridDim.x;
-    const uint64_t b0 = (lin % gridDim.x) * 256, b = b0 + tid;
+    // XCD-chunked tile order (xcd.h), for the point counts up to 16 (the benchmarked sizes; the wide
+    // instantiations keep the natural order's code unchanged)
+    uint32_t tile = blockIdx.x, vy = blockIdx.y;
+    if constexpr (MMAX <= 16) {
+        if (xcd) xcd_block_xy(&tile, &vy);
+    }
+    const uint64_t b0 = (uint64_t)tile * 256, b = b0 + tid;
     const bool live = b < B;
-    const uint64_t vec = lin / gridDim.x;
+    const uint64_t vec = vy;
     const int64_t* sh = shares + vec * (uint64_t)n_idx * B + (live ? b : B - 1);
     int64_t* o = out + vec * D;
     const uint32_t m = FULL ? (uint32_t)MMAX : n_idx + 1;
@@ -402,10 +406,13 @@ __global__ __launch_bounds__(256) void packed_reveal_canon_kernel(const int64_t*
                                                                   const uint32_t* __restrict__ tab, MontP M, int xcd) {
     extern __shared__ int64_t lds_o[];
     const uint32_t tid = threadIdx.x;
-    const uint64_t lin = xcd ? xcd_linear_block() : blockIdx.x + (uint64_t)blockIdx.y * gridDim.x;
-    const uint64_t b0 = (lin % gridDim.x) * 256, b = b0 + tid;
+    uint32_t tile = blockIdx.x, vy = blockIdx.y;
+    if constexpr (NMAX <= 16) {
+        if (xcd) xcd_block_xy(&tile, &vy);
+    }
+    const uint64_t b0 = (uint64_t)tile * 256, b = b0 + tid;
     const bool live = b < B;
-    const uint64_t vec = lin / gridDim.x;
+    const uint64_t vec = vy;
     const int64_t* sh = shares + vec * (uint64_t)n_idx * B + (live ? b : B - 1);
     int64_t* o = out + vec * D;
     const uint32_t p = M.p;
@@ -457,7 +464,7 @@ hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32
     dim3 grid((unsigned)((B + 255) / 256), (unsigned)a.n_vectors);
     const bool staged = k <= 16;                      // LDS stage: 256 * k * 8 B <= 32 KiB
     const size_t lds = staged ? (size_t)256 * k * sizeof(int64_t) : 0;
-    const int xcd = xcd_order_enabled() ? 1 : 0;
+    const int xcd = xcd_order_enabled() && (uint64_t)grid.x * grid.y < (1ull << 32) ? 1 : 0;
     if (mode == 0) {
         bool done = false;
         if constexpr (MM <= 16) {

@@ -9,6 +9,7 @@ one device).  Rank 0 writes every result to $SDA_MR_OUT (.npz); the parent compa
 """
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -61,6 +62,27 @@ def main():
         out2 = torch.empty(D, dtype=torch.int64, device=dev)
         Dd.combine_tiles_sharded(eng, m, tiles, D, D, part, out2)
         res[f"tiles_{name}_{N}x{D}"] = out2.cpu().numpy()
+        del mine
+
+    if backend == "nccl":
+        # a non-negative split step makes no blocking host read: with ~0.1 s of GPU work queued ahead of
+        # it, the deferred step (pass 1, RCCL all-reduce, finalize, async flag copy) returns to the host
+        # long before that work ends, its ticket still pending; finish() then yields the exact result
+        N, D = 64, 100_003
+        mine = torch.from_numpy(synth.fill(N, D, 0x5DA + 23, 0, MOD)).to(dev)
+        part = torch.empty(D, dtype=torch.int64, device=dev)
+        out = torch.empty(D, dtype=torch.int64, device=dev)
+        Dd.combine_rows_sharded(eng, MOD, mine.data_ptr(), N, D, D, part, out)      # warm the caches
+        torch.cuda.synchronize()
+        torch.cuda._sleep(200_000_000)
+        t0 = time.perf_counter()
+        tk = Dd.combine_rows_sharded(eng, MOD, mine.data_ptr(), N, D, D, part, out, defer=True)
+        res["deferred_host_s"] = np.array(time.perf_counter() - t0)
+        res["deferred_pending"] = np.array(not tk.done())
+        tk.finish()
+        t1 = time.perf_counter()
+        res["deferred_wait_s"] = np.array(t1 - t0)
+        res["deferred_out"] = out.cpu().numpy()
         del mine
 
     # recipient's ChaCha mask combine, seeds split over the ranks + one reduce

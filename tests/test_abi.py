@@ -68,3 +68,15 @@ def test_engine_fails_loudly_without_device():
     with pytest.raises(E.SdaError) as ei:
         E.Engine(0)
     assert ei.value.status in (E.ERR_DEVICE, E.ERR_INVALID_ARGUMENT)
+
+
+def test_every_entry_point_opens_a_call_scope():
+    """engine.cpp: every sda_status entry point starts with SDA_ENTRY (the RAII CallScope that ends the
+    call's stream-ordering scope on every return path), so no entry point can leave a stale
+    stream behind for the next call's early fail()."""
+    import re
+    src = open(os.path.join(ROOT, "sda_amd", "csrc", "engine.cpp")).read()
+    defs = list(re.finditer(r"^sda_status (sda_\w+)\([^)]*\)\s*\{\n(.*)\n", src, flags=re.M))
+    assert len(defs) >= 30
+    missing = [m.group(1) for m in defs if m.group(2).strip() != "SDA_ENTRY;"]
+    assert not missing, missing

@@ -4,6 +4,8 @@ Reference: client/src/crypto/encryption/sodium.rs:36-41 (encode), :82-88 (decode
 integer-encoding 1.0 VarInt for i64 (zigzag + LEB128; third-party, restated in the oracle and
 pinned by the protobuf sint64 known answers in test_oracle_golden.py).  Bit-exact.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -100,6 +102,15 @@ def test_clerk_decode_combine(engine, oracle):
         engine.clerk_decode_combine(S.Additive(3, m), bad)
     assert ei.value.status == 3
     assert engine.clerk_decode_combine(S.Additive(3, m), []).size == 0
+    # m = 0: blob 0 is folded before blob 1's length is checked (combiner.rs:20-25) -> the panic wins
+    for path in ("slots", "matrix"):
+        os.environ["SDA_CODEC_PATH"] = path
+        try:
+            with pytest.raises(SdaError) as ei:
+                engine.clerk_decode_combine(S.Additive(3, 0), bad)
+            assert ei.value.status == E.ERR_PRECONDITION, path
+        finally:
+            os.environ.pop("SDA_CODEC_PATH", None)
 
 
 def test_clerk_decode_combine_dev_and_encode_dev(engine, oracle):

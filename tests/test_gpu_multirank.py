@@ -74,6 +74,19 @@ def test_sharded_rows_and_tiles_equal_single_pass(results, oracle, name, N, D, m
     assert np.array_equal(results[f"tiles_{name}_{N}x{D}"], exp)
 
 
+def test_split_step_makes_no_blocking_host_read(results, oracle):
+    """rccl_world1: the non-negative participation-split step (defer=True) returns to the host while
+    ~0.1 s of earlier GPU work is still running -- no host read between its RCCL all-reduce and its
+    finalize -- and its ticket's finish() then gives the exact result."""
+    if "deferred_out" not in results:
+        pytest.skip("RCCL case only")
+    host_s, wait_s = float(results["deferred_host_s"]), float(results["deferred_wait_s"])
+    assert bool(results["deferred_pending"]), "the step's flags were already on the host: it waited"
+    assert host_s < wait_s / 2, (host_s, wait_s)
+    x = synth.fill(64, 100_003, 0x5DA + 23, 0, W.MOD)
+    assert np.array_equal(results["deferred_out"], oracle.combine(W.MOD, x))
+
+
 def test_sharded_mask_combine_seed_split(results, oracle):
     """mask_combine_sharded: the recipient's ChaCha mask combine over seeds split across ranks."""
     exp = oracle.chacha_mask_combine(W.MOD, 70_001, W.SEEDS)
@@ -112,6 +125,7 @@ def test_bench_spawns_its_own_ranks(tmp_path):
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["value"] > 0
+    assert rec["dist"]["world_size"] == 2 and [r["rank"] for r in rec["dist"]["ranks"]] == [0, 1]
     assert rec["combine_signed_split"]["passes"] == 2
     bad = subprocess.run(cmd, env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), capture_output=True,
                          text=True, timeout=120)

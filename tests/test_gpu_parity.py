@@ -108,6 +108,17 @@ def test_combine_negative_modulus_and_errors(engine, oracle):
     with pytest.raises(SdaError) as ei:
         engine.share_combine(S.Additive(3, 0), [[1, 2]])
     assert ei.value.status == E.ERR_PRECONDITION
+    # m = 0 with a later row of another length: combiner.rs:20-25 folds row 0 first, so `%= 0` panics
+    # before row 1's length is checked; with an empty row 0 nothing is folded and the length check wins
+    with pytest.raises(SdaError) as ei:
+        engine.share_combine(S.Additive(3, 0), [[1, 2], [3]])
+    assert ei.value.status == E.ERR_PRECONDITION
+    with pytest.raises(SdaError) as ei:
+        engine.share_combine(S.Additive(3, 0), [[], [3]])
+    assert ei.value.status == E.ERR_WRONG_DIMENSION
+    with pytest.raises(SdaError) as ei:
+        engine.secret_reconstruct(S.Additive(3, 0), 2, [(0, [1, 2]), (1, [1])])
+    assert ei.value.status == E.ERR_PRECONDITION
 
 
 def test_additive_reconstruct_is_combine(engine, oracle):

@@ -154,6 +154,38 @@ __global__ __launch_bounds__(BS) void gen_mem(const int64_t* __restrict__ sec, c
     }
 }
 
+// Memory-only model of the reveal (packed_reveal.hip): a lane reads its batch's NI shares from the
+// [V][NI][B] clerk rows (1 MB apart) and writes the batch's K secrets; the workgroup's 256 x K results go
+// through LDS so the [V][D] output is written with coalesced 16-byte stores (the reveal's STAGED flush).
+constexpr int NI = 15;
+template <bool NT_LOAD, bool XCD>
+__global__ __launch_bounds__(BS) void reveal_mem(const int64_t* __restrict__ sh, int64_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) int64_t lds[BS * K];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t total = (uint64_t)gridDim.x * gridDim.y;
+    uint64_t L = blockIdx.x + (uint64_t)blockIdx.y * gridDim.x;
+    if (XCD) {
+        const uint64_t q = total / 8, r = total % 8, x = L % 8;
+        L = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + L / 8;
+    }
+    const uint64_t vec = L / gridDim.x, tile = L % gridDim.x;
+    const uint64_t b0 = tile * BS, b = b0 + tid;
+    const uint64_t nb = std::min<uint64_t>(BS, B - b0);
+    const int64_t* src = sh + vec * NI * B + (b < B ? b : B - 1);
+    int64_t v[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) v[i] = NT_LOAD ? __builtin_nontemporal_load(src + (uint64_t)i * B) : src[(uint64_t)i * B];
+    int64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) acc ^= v[i];
+#pragma unroll
+    for (int e = 0; e < K; ++e) lds[tid * K + e] = acc + e;
+    __syncthreads();
+    v2l* o = reinterpret_cast<v2l*>(out + vec * D + b0 * K);
+    const v2l* l2 = reinterpret_cast<const v2l*>(lds);
+    for (uint32_t j = tid; j < nb * K / 2; j += BS) __builtin_nontemporal_store(l2[j], o + j);
+}
+
 __global__ __launch_bounds__(256) void copy_flat(const v2l* __restrict__ src, v2l* __restrict__ dst, uint64_t n) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
@@ -257,10 +289,25 @@ int main(int argc, char** argv) {
     GEN(0, 0, 2, 0, 0, "ld8, permlane x4 sc1");
     GEN(0, 0, 3, 0, 0, "ld8, permlane x4 sc0 sc1 nt");
     GEN(0, 0, 0, 1, 0, "ld8, permlane x4 nt, XCD-chunked");
+    GEN(1, 0, 0, 1, 0, "ld16, permlane x4 nt, XCD-chunked");
+    GEN(0, 1, 0, 1, 0, "ld8, 1 KiB rows nt, XCD-chunked");
+    GEN(2, 0, 0, 1, 0, "LDS-DMA, permlane x4 nt, XCD-chunked");
+    GEN(0, 0, 1, 1, 0, "ld8, permlane x4 plain, XCD-chunked");
     GEN(0, 0, 0, 0, 1, "ld8, permlane x4 nt, rows rotated");
     GEN(1, 1, 0, 0, 1, "ld16, 1 KiB rows nt, rows rotated");
     GEN(1, 1, 2, 0, 0, "ld16, 1 KiB rows sc1");
     GEN(1, 1, 1, 0, 0, "ld16, 1 KiB rows plain");
+    {   // reveal pattern: V x 15 share rows in, V x D secrets out (reuses the share-gen buffers)
+        const double rbytes = (double)V * NI * B * 8 + (double)V * D * 8;
+        int64_t* rsh = out;           // [V][NI][B] fits in [V][NR][B]
+        int64_t* rout = sec;          // [V][D]
+        timeit("reveal mem: nt loads, natural order", rbytes,
+               [&] { hipLaunchKernelGGL((reveal_mem<true, false>), grid, blk, 0, 0, rsh, rout); }, reps);
+        timeit("reveal mem: nt loads, XCD-chunked", rbytes,
+               [&] { hipLaunchKernelGGL((reveal_mem<true, true>), grid, blk, 0, 0, rsh, rout); }, reps);
+        timeit("reveal mem: plain loads, XCD-chunked", rbytes,
+               [&] { hipLaunchKernelGGL((reveal_mem<false, true>), grid, blk, 0, 0, rsh, rout); }, reps);
+    }
     timeit("write-only rows (no reads)", (double)ob, [&] { hipLaunchKernelGGL(write_rows, grid, blk, 0, 0, out); }, reps);
     const uint64_t n16 = ob / 16 / 2;
     timeit("copy 1:1 flat (read + write bytes)", (double)n16 * 32,
