@@ -471,6 +471,7 @@ def main():
                 "check": "bit-exact on 256 sampled columns: the reference recurrence over all ranks' rows in order"}
             log(f"[combine_signed_split] {json.dumps(side['combine_signed_split'])}")
         del shares
+        torch.cuda.empty_cache()         # the next leg gets fresh allocations, not a reused segment
 
     # ---------------- side legs (rank-local, reported by rank 0) ----------------
     if not args.no_side and args.only in (None, "shamir"):
@@ -552,6 +553,7 @@ def main():
             side["shamir"]["n_gpus"] = world
         log(f"[shamir] {json.dumps(side['shamir'])}")
         del sec, drw, sh, sub, rev
+        torch.cuda.empty_cache()         # the next leg gets fresh allocations, not a reused segment
     if not args.no_side and args.only in (None, "chacha"):
         Dc, Ns = 1_000_000, args.chacha_seeds
         seeds = torch.randint(0, 2**31 - 1, (Ns, 4), dtype=torch.int32, device=dev,
@@ -653,6 +655,7 @@ def main():
         }
         log(f"[codec] {json.dumps(side['codec'])}")
         del x, buf, mat
+        torch.cuda.empty_cache()         # the next leg gets fresh allocations, not a reused segment
 
     if not args.no_side and args.only in (None, "snapshot"):
         # server side (stores.rs:86-101): a snapshot of Ps participations x 26 clerk payloads of
@@ -695,6 +698,7 @@ def main():
         }
         log(f"[snapshot] {json.dumps(side['snapshot'])}")
         del src, dst
+        torch.cuda.empty_cache()         # the next leg gets fresh allocations, not a reused segment
 
     if not args.no_side and args.only in (None, "pipelines"):
         # configs[4] per GPU: participant = ChaCha mask -> packed share-gen -> per-clerk payload encoding
