@@ -33,7 +33,6 @@
 #include <type_traits>
 
 #include "kernels.h"
-#include "xcd.h"
 
 namespace sda {
 
@@ -129,29 +128,17 @@ __device__ __forceinline__ Window interior_window(uint32_t cm) {
 
 // 2-D grid: blockIdx.y = blob (+ y0), blockIdx.x = region within the blob (16 KiB aligned to the
 // byte buffer).  Blocks past a blob's last region exit at once (payload blobs have near-equal sizes).
-// SDA_CODEC_XCD (build-time A/B knob, default on): the (region, blob) grid in XCD-chunked order (xcd.h), so
-// one XCD streams consecutive regions of the same blobs.
-#ifndef SDA_CODEC_XCD
-#define SDA_CODEC_XCD 1
-#endif
-__device__ __forceinline__ void grid_xy(uint64_t* bx, uint64_t* by) {
-    uint32_t x = blockIdx.x, y = blockIdx.y;
-    if (SDA_CODEC_XCD) xcd_block_xy(&x, &y);      // codec grids hold < 2^32 workgroups (host plans)
-    *bx = x;
-    *by = y;
-}
-
 __device__ __forceinline__ bool region_of(const uint64_t* __restrict__ blob_region,
                                           const uint64_t* __restrict__ blob_off, uint32_t y0, uint32_t* blob,
                                           uint64_t* region, uint64_t* word) {
-    uint64_t bx, by;
-    grid_xy(&bx, &by);
-    const uint32_t b = y0 + (uint32_t)by;
+    // (natural order: the XCD-chunked order of xcd.h made the clerk's decode -> combine 3 % slower,
+    // profiles/r04f)
+    const uint32_t b = y0 + blockIdx.y;
     const uint64_t r0 = blob_region[b], r1 = blob_region[b + 1];
-    if (r0 + bx >= r1) return false;
+    if (r0 + blockIdx.x >= r1) return false;
     *blob = b;
-    *region = r0 + bx;
-    *word = (blob_off[b] / kRegionBytes + bx) * (kRegionBytes / 16);
+    *region = r0 + blockIdx.x;
+    *word = (blob_off[b] / kRegionBytes + blockIdx.x) * (kRegionBytes / 16);
     return true;
 }
 
@@ -519,7 +506,7 @@ __global__ __launch_bounds__(kThreads) void slot_combine_kernel(const int32_t* _
     constexpr uint32_t kTile = CPL * kThreads;
     const uint64_t dim = *dim_p;
     if (*flags || dim > out_cap) return;
-    // natural order: the XCD-chunked order made this read-only walk 1.6x slower (profiles/r04d)
+    // natural order: the XCD-chunked order (xcd.h) made this read-only walk 1.6x slower (profiles/r04d)
     const uint64_t tile = blockIdx.x;
     const uint64_t e0 = tile * kTile;
     const uint32_t o = CPL * threadIdx.x;
@@ -852,9 +839,7 @@ __device__ __forceinline__ bool enc_pairs_ok(const int64_t* rowp, uint64_t e0, u
 __global__ __launch_bounds__(kThreads) void varint_size_kernel(const int64_t* __restrict__ vals, uint64_t len,
                                                                uint64_t stride, uint32_t chunks,
                                                                uint64_t* __restrict__ chunk_bytes) {
-    uint64_t bx_, by_;
-    grid_xy(&bx_, &by_);                        // XCD-chunked (chunk, row) order
-    const uint32_t c = (uint32_t)bx_, row = (uint32_t)by_;
+    const uint32_t c = blockIdx.x, row = blockIdx.y;
     const uint64_t e0 = (uint64_t)c * kEncChunk;
     const int64_t* rowp = vals + (uint64_t)row * stride;
     uint64_t n = 0;
@@ -904,9 +889,7 @@ __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* _
                                                                 const uint64_t* __restrict__ row_base,
                                                                 const uint32_t* __restrict__ too_big,
                                                                 uint8_t* __restrict__ dst) {
-    uint64_t bx_, by_;
-    grid_xy(&bx_, &by_);                        // XCD-chunked (chunk, row) order
-    const uint32_t c = (uint32_t)bx_, row = (uint32_t)by_;
+    const uint32_t c = blockIdx.x, row = blockIdx.y;
     if (*too_big) return;
     const uint64_t e0 = (uint64_t)c * kEncChunk;
     constexpr uint32_t kBufQuads = (kEncChunk * 10 + 32) / 16;      // lead < 16, + the shifted tail dwords

@@ -115,6 +115,9 @@ __device__ __forceinline__ void gen_store(const V& v, V* a) {
 template <int L>
 constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
 
+#ifndef SDA_GEN_FULLTILE
+#define SDA_GEN_FULLTILE 1
+#endif
 #ifndef SDA_GEN_WAVES
 #define SDA_GEN_WAVES 4
 #endif
@@ -238,7 +241,21 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         // ---- stage the tile's inputs through LDS with coalesced loads ----
         // lds[0, BS k): the secrets of batches b0.. (zero past D: batched.rs:37-43 pads the tail
         // batch); lds[BS k, BS (k + t)): their randomness.  U loads in flight before the first wait.
-        {
+        // uniform: no tail batch, no padding (SDA_GEN_FULLTILE = 0, a build-time A/B knob, stages every tile
+        // through the bounds-checked loops)
+        const bool full = SDA_GEN_FULLTILE && b0 + BS <= B && (b0 + BS) * k <= D;
+        if (full) {
+            // the tile's BS (k + t) = BS (L - 1) input words as L - 1 rows of BS: row u < k is secrets
+            // [b0 k + u BS, +BS), row u >= k draws [(vec B + b0) t + (u - k) BS, +BS) -- each row one
+            // coalesced load from a uniform base, landing at lds[u BS + tid] (the layout below)
+            const int64_t* ssrc = sec + b0 * k + tid;
+            const int64_t* dsrc = draws + ((uint64_t)vec * B + b0) * t + tid;
+            int64_t v[L - 1];
+            static_for<0, L - 1>([&](auto u) {
+                v[u] = gen_load((uint32_t)u < k ? ssrc + (uint64_t)u * BS : dsrc + (uint64_t)(u - k) * BS);
+            });
+            static_for<0, L - 1>([&](auto u) { lds[lpos((uint32_t)u * BS + tid)] = v[u]; });
+        } else {
             constexpr int U = 8;
             const uint64_t nb = B - b0 < (uint64_t)BS ? B - b0 : (uint64_t)BS;
             const uint64_t s0 = b0 * k;
@@ -281,7 +298,8 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         {
             const uint32_t es = lb * k - 1;                                    // + i,      i <= k
             const uint32_t ed = (uint32_t)BS * k + lb * t - 1 - k;             // + i,      i >  k
-            static_for<1, L>([&](auto i) { raw[i] = live ? lds[lpos(((uint32_t)i <= k ? es : ed) + i)] : 0; });
+            // (lanes past B read whatever the LDS holds: they log nothing and store nothing)
+            static_for<1, L>([&](auto i) { raw[i] = lds[lpos(((uint32_t)i <= k ? es : ed) + i)]; });
         }
         bool in_range = true;
         static_for<1, L>([&](auto i) { in_range = in_range && ((uint64_t)(raw[i] + (P - 1)) < (uint64_t)(2 * P - 1)); });
