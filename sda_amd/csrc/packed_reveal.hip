@@ -157,69 +157,6 @@ __device__ __forceinline__ bool newton_reveal_signbit(FE (&s)[MMAX], uint32_t m,
     return zt.bad();
 }
 
-#ifndef SDA_REVEAL_PAIR
-#define SDA_REVEAL_PAIR 0                // build-time A/B knob: two batches per lane, in lockstep
-#endif
-#if SDA_REVEAL_PAIR
-// The sign-bit reveal of TWO batches (points s and q, all MMAX of them) in lockstep, statement by statement,
-// so every dependent Montgomery chain has an independent partner in the same basic block (the A/B asked in
-// VERDICT r03 item 5).  Same arithmetic as newton_reveal_signbit<MMAX, KU, true>.
-template <int MMAX, int KU>
-__device__ __forceinline__ void newton_reveal_signbit_x2(FE (&s)[MMAX], FE (&q)[MMAX], uint32_t k,
-                                                         const uint32_t* __restrict__ tab, const MontP& M,
-                                                         int64_t* ds, int64_t* dq, bool* bad_s, bool* bad_q) {
-    const uint32_t p = M.p;
-    ZeroTrap zs, zq;
-#define SDA_NSTEP(V, ZT)                                                         \
-    do {                                                                         \
-        uint32_t fc, n;                                                          \
-        if constexpr (i == 1) {                                                  \
-            fc = montu<false>(a_m, V[1].c, M);                                   \
-            n = (uint32_t)V[1].s;                                                \
-        } else {                                                                 \
-            const uint32_t d = V[i].c - V[i - 1].c;                              \
-            fc = montu<false>(a_m, d + p, M);                                    \
-            n = maj3_nb((uint32_t)V[i].s, (uint32_t)V[i - 1].s, d);              \
-        }                                                                        \
-        V[i] = FE{(int32_t)n, fc};                                               \
-        ZT.note1(fc);                                                            \
-    } while (0)
-    static_for<1, MMAX>([&](auto j) {
-        static_for<0, MMAX - j>([&](auto ii) {
-            constexpr int i = MMAX - 1 - ii;
-            const uint32_t a_m = tab[OFF_INVM + j * TS + i];
-            SDA_NSTEP(s, zs);
-            SDA_NSTEP(q, zq);
-        });
-    });
-#undef SDA_NSTEP
-    auto eval = [&](uint32_t e) __attribute__((always_inline)) {
-        const uint32_t* np = tab + OFF_NP + e * TS;
-        const uint32_t* npm = tab + OFF_NPM + e * TS;
-        uint32_t pcs = 0, ns = 0, pcq = 0, nq = 0;
-        static_for<1, MMAX>([&](auto i) {
-            const uint32_t tcs = montu<false>(npm[i], s[i].c, M), tcq = montu<false>(npm[i], q[i].c, M);
-            const uint32_t sts = (uint32_t)s[i].s ^ np[i], stq = (uint32_t)q[i].s ^ np[i];
-            if constexpr (i == 1) {
-                pcs = tcs; ns = sts; pcq = tcq; nq = stq;
-            } else {
-                const uint32_t ys = pcs + tcs, yq = pcq + tcq;
-                const uint32_t dys = ys - p, dyq = yq - p;
-                pcs = min(ys, dys); pcq = min(yq, dyq);
-                ns = maj3(ns, sts, dys); nq = maj3(nq, stq, dyq);
-                zs.note1(pcs); zq.note1(pcq);
-            }
-        });
-        zs.flush(); zq.flush();
-        ds[e] = (int32_t)(pcs - (p & (uint32_t)((int32_t)ns >> 31)));
-        dq[e] = (int32_t)(pcq - (p & (uint32_t)((int32_t)nq >> 31)));
-    };
-    static_for<0, KU>([&](auto e) { if ((uint32_t)e < k) eval((uint32_t)e); });
-    *bad_s = zs.bad();
-    *bad_q = zq.bad();
-}
-#endif
-
 template <int MMAX, int KU, bool LAZY, bool FULL>
 __device__ __forceinline__ bool newton_reveal(FE (&s)[MMAX], uint32_t m, uint32_t k, const uint32_t* __restrict__ tab,
                                               const MontP& M, int64_t* dst, uint32_t lim) {
@@ -316,45 +253,6 @@ __global__ __launch_bounds__(256) void packed_reveal_exact_kernel(const int64_t*
     }
     reveal_flush<STAGED>(lds_o, o, b0, B, D, k);
 }
-
-#if SDA_REVEAL_PAIR
-// packed_reveal_exact_kernel<MMAX, true, 8, true, true> with two batches per lane: lane t of tile x takes
-// batches 512 x + t and 512 x + 256 + t; the tile's 512 x k results leave through LDS.
-template <int MMAX>
-__global__ __launch_bounds__(256) void packed_reveal_exact_pair_kernel(const int64_t* __restrict__ shares, uint64_t B,
-                                                                       uint64_t D, int64_t* __restrict__ out,
-                                                                       uint32_t n_idx, uint32_t k,
-                                                                       const uint32_t* __restrict__ tab, MontP M,
-                                                                       unsigned int* __restrict__ log, int xcd) {
-    extern __shared__ int64_t lds_o[];
-    const uint32_t tid = threadIdx.x;
-    uint32_t tile = blockIdx.x, vy = blockIdx.y;
-    if (xcd) xcd_block_xy(&tile, &vy);
-    const uint64_t b0 = (uint64_t)tile * 512, bs = b0 + tid, bq = b0 + 256 + tid;
-    const bool ls = bs < B, lq = bq < B;
-    const uint64_t vec = vy;
-    const int64_t* base = shares + vec * (uint64_t)n_idx * B;
-    int64_t* o = out + vec * D;
-    FE s[MMAX], q[MMAX];
-    const bool ins = load_points<MMAX, true>(base + (ls ? bs : B - 1), B, MMAX, M.p, s);
-    const bool inq = load_points<MMAX, true>(base + (lq ? bq : B - 1), B, MMAX, M.p, q);
-    bool bad_s, bad_q;
-    newton_reveal_signbit_x2<MMAX, 8>(s, q, k, tab, M, lds_o + tid * k, lds_o + (256 + tid) * k, &bad_s, &bad_q);
-    if ((!ins || bad_s) && ls) {
-        const uint32_t slot = atomicAdd(log, 1u);
-        if (slot < kGenLogCap) reinterpret_cast<uint64_t*>(log + 16)[slot] = vec * B + bs;
-    }
-    if ((!inq || bad_q) && lq) {
-        const uint32_t slot = atomicAdd(log, 1u);
-        if (slot < kGenLogCap) reinterpret_cast<uint64_t*>(log + 16)[slot] = vec * B + bq;
-    }
-    __syncthreads();
-    const uint64_t first = b0 * k;
-    const uint64_t last = (b0 + 512 < B ? b0 + 512 : B) * k;
-    const uint32_t cnt = (uint32_t)((last < D ? last : D) - first);
-    for (uint32_t j = tid; j < cnt; j += 256) o[first + j] = lds_o[j];
-}
-#endif
 
 // Generic exact reveal of one batch (shares outside (-p, p)): tss' Newton divided differences and
 // evaluation with wrapping i64 arithmetic and truncated `%`, reading the batch's shares from global
@@ -571,12 +469,6 @@ hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32
         bool done = false;
         if constexpr (MM <= 16) {
             done = staged && k <= 8;
-#if SDA_REVEAL_PAIR
-            if (done && M.p >= kLazyTruncMinP && n_idx + 1 == MM && MM == 16)
-                hipLaunchKernelGGL((packed_reveal_exact_pair_kernel<MM>), dim3((unsigned)((B + 511) / 512), grid.y),
-                                   dim3(256), 2 * lds, s, a.shares, B, a.dimension, a.out, n_idx, k, tab, M, log, xcd);
-            else
-#endif
             if (done && M.p >= kLazyTruncMinP && n_idx + 1 == MM)
                 hipLaunchKernelGGL((packed_reveal_exact_kernel<MM, true, 8, true, true>), grid, dim3(256), lds, s,
                                    a.shares, B, a.dimension, a.out, n_idx, k, tab, M, log, xcd);
