@@ -148,8 +148,12 @@ template <bool LAZY, bool DIRECT, bool PRE>
 __device__ __forceinline__ void chacha_tile(const uint32_t* __restrict__ seeds, uint32_t w, uint64_t s0, uint64_t s1,
                                             uint64_t x, uint64_t D, unsigned long long* __restrict__ acc,
                                             const Mod64& M, uint64_t zone, uint64_t r64, const RejectLog& log,
-                                            const ChachaPre* __restrict__ pre, unsigned long long* st) {
-    const uint32_t tid = threadIdx.x;
+                                            const ChachaPre* __restrict__ pre, unsigned long long* st,
+                                            bool opaque_tid = false) {
+    uint32_t tid = threadIdx.x;
+    // inside the stream-K run loop: an opaque lane id, so that no per-lane value is hoisted out of the loop
+    // and held across runs (the hoisted form held 94 VGPRs instead of 80)
+    if (opaque_tid) asm volatile("" : "+v"(tid));
     const uint64_t blk = x * 256 + tid;
     const uint64_t n_blk = (D + 7) / 8;
     const bool live = blk < n_blk;
@@ -265,7 +269,10 @@ __global__ __launch_bounds__(256) void chacha_combine_kernel(const uint32_t* __r
 // bench shape (489 tiles x 256 seeds, 1,792 resident workgroups) it launched 1,956 of them, a second
 // round 9 % full behind the first.  Here every workgroup ends within one unit of the others.
 template <bool LAZY, bool PRE>
-__global__ __launch_bounds__(256) void chacha_combine_sk_kernel(const uint32_t* __restrict__ seeds, uint32_t w,
+#ifndef SDA_CHACHA_SK_WAVES
+#define SDA_CHACHA_SK_WAVES 6                  // waves per SIMD the stream-K kernel is built for (80 VGPRs)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDA_CHACHA_SK_WAVES, 8))) void chacha_combine_sk_kernel(const uint32_t* __restrict__ seeds, uint32_t w,
                                                                 uint64_t n_seeds, uint64_t q, uint64_t r, uint64_t D,
                                                                 unsigned long long* __restrict__ acc, Mod64 M,
                                                                 uint64_t zone, uint64_t r64, RejectLog log,
@@ -277,11 +284,11 @@ __global__ __launch_bounds__(256) void chacha_combine_sk_kernel(const uint32_t* 
     uint64_t x = u / n_seeds, s0 = u - x * n_seeds;   // the first run's tile and seed (one division)
     while (left) {
         const uint64_t s1 = n_seeds - s0 < left ? n_seeds : s0 + left;
-        chacha_tile<LAZY, false, PRE>(seeds, w, s0, s1, x, D, acc, M, zone, r64, log, pre, st);
-        __syncthreads();                          // st is rewritten by the next run
+        chacha_tile<LAZY, false, PRE>(seeds, w, s0, s1, x, D, acc, M, zone, r64, log, pre, st, true);
         left -= s1 - s0;
         ++x;
         s0 = 0;
+        if (left) __syncthreads();                // st is rewritten by the next run
     }
 }
 
