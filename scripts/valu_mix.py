@@ -31,7 +31,7 @@ KERNELS = [
     ("gen_canonical", "packed_gen.hip", "SDA_GEN_PART=27", "packed_gen_kernelILi16ELi27ELb1ELb1ELb0ELb0E"),
     ("reveal_exact", "packed_reveal.hip", "SDA_REVEAL_PART=16", "packed_reveal_exact_kernelILi16ELb1ELi8ELb1ELb1E"),
     ("reveal_canonical", "packed_reveal.hip", "SDA_REVEAL_PART=16", "packed_reveal_canon_kernelILi16ELb1E"),
-    ("chacha_combine", "chacha.hip", None, "chacha_combine_kernelILb1ELb0ELb1E"),
+    ("chacha_combine", "chacha.hip", None, "chacha_combine_sk_kernelILb1ELb1E"),
 ]
 # the PMC report's short names for the same kernels
 PMC_NAMES = {
@@ -39,7 +39,7 @@ PMC_NAMES = {
     "gen_canonical": "packed_gen_kernel<16, 27, true, true, false, false>",
     "reveal_exact": "packed_reveal_exact_kernel<16, true, 8, true, true>",
     "reveal_canonical": "packed_reveal_canon_kernel<16, true>",
-    "chacha_combine": "chacha_combine_kernel<true, false, true>",
+    "chacha_combine": "chacha_combine_sk_kernel<true, true>",
 }
 
 # ChaCha20 blocks of the counted launch (bench.py's chacha leg: 256 seeds x 1M-dim, 8 draws per block)

@@ -483,7 +483,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         const uint64_t pb = b0 + pb_off;
         const bool st1 = pair_ok && pb + 1 < B;
         int64_t* orow = out + ((uint64_t)vec * NR + half) * B + pb;
-        if constexpr (WIDE && SDA_GEN_LDS_STORE && NR <= 2 * (L - 1)) {
+        if constexpr (WIDE && SDA_GEN_LDS_STORE && L <= 16 && BS % 128 == 0 && NR <= 2 * (L - 1)) {
             // through LDS, one clerk row per store instruction: the tile's NR x BS shares (as int32, 4 NR BS
             // bytes <= the 8 (L - 1) BS of the input stage) transposed to [row][batch]; each wave then stores
             // whole 1 KiB pieces (128 batches of one row).  The pair flags travel alongside.
