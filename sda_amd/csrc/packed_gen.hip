@@ -115,9 +115,6 @@ __device__ __forceinline__ void gen_store(const V& v, V* a) {
 template <int L>
 constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
 
-#ifndef SDA_GEN_LDS_STORE
-#define SDA_GEN_LDS_STORE 1            // build-time A/B knob: shares leave through an LDS transpose
-#endif
 #ifndef SDA_GEN_FULLTILE
 #define SDA_GEN_FULLTILE 1
 #endif
@@ -226,8 +223,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
     // word per 16 keeps the even/odd lane->batch reads below 2-way bank conflicted (b64 optimum).
     // (Unpadded at 5 waves/EU: 5 tiles of <= 31.75 KiB fit the 160 KiB LDS; the pad measured neutral.)
     constexpr bool PAD = gen_waves<L, CANON, LAZY>() < 5;
-    __shared__ __attribute__((aligned(16))) int64_t lds[BS * (L - 1) + (PAD ? BS * (L - 1) / 16 + 1 : 0)];
-    __shared__ uint32_t okw[SDA_GEN_LDS_STORE ? BS / 2 : 1];   // per batch pair: both in range, no trap
+    __shared__ int64_t lds[BS * (L - 1) + (PAD ? BS * (L - 1) / 16 + 1 : 0)];
     auto lpos = [](uint32_t e) { return PAD ? e + (e >> 4) : e; };
 
     {
@@ -483,32 +479,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         const uint64_t pb = b0 + pb_off;
         const bool st1 = pair_ok && pb + 1 < B;
         int64_t* orow = out + ((uint64_t)vec * NR + half) * B + pb;
-        if constexpr (WIDE && SDA_GEN_LDS_STORE && L <= 16 && BS % 128 == 0 && NR <= 2 * (L - 1)) {
-            // through LDS, one clerk row per store instruction: the tile's NR x BS shares (as int32, 4 NR BS
-            // bytes <= the 8 (L - 1) BS of the input stage) transposed to [row][batch]; each wave then stores
-            // whole 1 KiB pieces (128 batches of one row).  The pair flags travel alongside.
-            __syncthreads();                                      // every lane has read its points
-            int32_t* l32 = reinterpret_cast<int32_t*>(lds);
-            static_for<1, N3>([&](auto j) { l32[(j - 1) * BS + lb] = ys[j]; });
-            if (!half) okw[pb_off / 2] = pair_ok ? 1u : 0u;
-            __syncthreads();
-            constexpr int NW = BS / 64, PER_ROW = BS / 128, PIECES = NR * PER_ROW;
-            const uint32_t wave = tid >> 6;
-            static_for<0, (PIECES + NW - 1) / NW>([&](auto i) {
-                const uint32_t pc = wave + (uint32_t)i * NW;
-                if (PIECES % NW == 0 || pc < PIECES) {
-                    const uint32_t row = pc / PER_ROW, bl = (pc % PER_ROW) * 128 + 2 * lane;
-                    typedef int32_t v2i __attribute__((ext_vector_type(2)));
-                    typedef int32_t v4i __attribute__((ext_vector_type(4)));
-                    const v2i v = *reinterpret_cast<const v2i*>(l32 + row * BS + bl);
-                    if (okw[bl / 2] && b0 + bl + 1 < B) {         // B even: the pair is whole
-                        v4i* d4 = reinterpret_cast<v4i*>(out + ((uint64_t)vec * NR + row) * B + b0 + bl);
-                        const v4i val = {v[0], v[0] >> 31, v[1], v[1] >> 31};
-                        gen_store(val, d4);
-                    }
-                }
-            });
-        } else if constexpr (WIDE) {       // B even => pb + 1 < B whenever pb < B
+        if constexpr (WIDE) {              // B even => pb + 1 < B whenever pb < B
             static_for<0, NR / 2>([&](auto q) {
                 const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)ys[1 + 2 * q], (uint32_t)ys[2 + 2 * q],
                                                                 false, false);
