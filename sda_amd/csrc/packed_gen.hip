@@ -1,8 +1,6 @@
 // packed_gen.hip -- packed-Shamir share generation (see packed_common.h for the algorithm).
 #include <stdlib.h>
 
-#include <type_traits>
-
 #include "packed_common.h"
 #include "xcd.h"
 
@@ -123,20 +121,10 @@ constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
 #ifndef SDA_GEN_WAVES
 #define SDA_GEN_WAVES 4
 #endif
-#ifndef SDA_GEN_LDS32
-#define SDA_GEN_LDS32 1                // build-time A/B knob: int32 input stage (6 waves) for canonical / lazy L <= 16
-#endif
-// The canonical and lazy-exact kernels at L <= 16, n + 1 <= 27 stage their inputs as int32 (every in-range input is one):
-// 15 KiB of LDS per tile instead of 30, so 6 tiles fit a CU and the transform's <= 80 VGPRs give 6 waves per
-// EU.  A tile holding an input outside (-p, p) (raw i64 secrets) reads its values from global memory instead.
-template <int L, int N3, bool CANON, bool LAZY>
-constexpr bool gen_lds32() { return SDA_GEN_LDS32 && L <= 16 && N3 <= 27 && (CANON || LAZY); }
-// Waves per EU: 6 with the int32 stage (8 for canonical, <= 64 VGPRs); 5 where the transform fits 102 VGPRs without spilling (canonical and
-// lazy-exact at L <= 16), else SDA_GEN_WAVES (4: 128 VGPRs).
-template <int L, int N3, bool CANON, bool LAZY>
-constexpr int gen_waves() {
-    return gen_lds32<L, N3, CANON, LAZY>() ? (CANON ? 8 : 6) : (L <= 16 && (CANON || LAZY)) ? 5 : SDA_GEN_WAVES;
-}
+// Waves per EU: 5 where the transform fits 102 VGPRs without spilling (canonical and lazy-exact at
+// L <= 16), else SDA_GEN_WAVES (4: 128 VGPRs).
+template <int L, bool CANON, bool LAZY>
+constexpr int gen_waves() { return (L <= 16 && (CANON || LAZY)) ? 5 : SDA_GEN_WAVES; }
 
 
 // CANONICAL share generation: the same transform in canonical residues [0, p) only -- no sign
@@ -215,7 +203,7 @@ __device__ __forceinline__ void transform_canon(const int64_t (&raw)[L], const G
 // words in SGPRs across tiles and spill.)
 template <int L, int N3, bool WIDE, bool CANON, bool LAZY, bool SIGNBIT = false>
 __global__ __launch_bounds__(gen_block<L>())
-__attribute__((amdgpu_waves_per_eu(gen_waves<L, N3, CANON, LAZY>(), gen_waves<L, N3, CANON, LAZY>())))
+__attribute__((amdgpu_waves_per_eu(gen_waves<L, CANON, LAZY>(), gen_waves<L, CANON, LAZY>())))
 void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const int64_t* __restrict__ draws,
                        int64_t* __restrict__ out, uint32_t k, uint32_t t, uint64_t B,
                        const GenTables* __restrict__ Tp, unsigned int* __restrict__ log, int xcd) {
@@ -234,17 +222,9 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
     // LDS word e (batch-major [batch][k] secrets, then [batch][t] draws) lives at lpos(e): one pad
     // word per 16 keeps the even/odd lane->batch reads below 2-way bank conflicted (b64 optimum).
     // (Unpadded at 5 waves/EU: 5 tiles of <= 31.75 KiB fit the 160 KiB LDS; the pad measured neutral.)
-    constexpr bool PAD = gen_waves<L, N3, CANON, LAZY>() < 5;
-    constexpr bool N32 = gen_lds32<L, N3, CANON, LAZY>();
-    using LT = typename std::conditional<N32, int32_t, int64_t>::type;
-    __shared__ LT lds[BS * (L - 1) + (PAD ? BS * (L - 1) / 16 + 1 : 0)];
-    __shared__ uint32_t wbad[N32 ? BS / 64 : 1];     // N32: a wave staged an input outside (-p, p)
+    constexpr bool PAD = gen_waves<L, CANON, LAZY>() < 5;
+    __shared__ int64_t lds[BS * (L - 1) + (PAD ? BS * (L - 1) / 16 + 1 : 0)];
     auto lpos = [](uint32_t e) { return PAD ? e + (e >> 4) : e; };
-    bool stage_ok = true;                            // N32: every input this lane staged is in (-p, p)
-    auto put = [&](uint32_t e, int64_t v) __attribute__((always_inline)) {
-        if constexpr (N32) stage_ok = stage_ok && (uint64_t)(v + (P - 1)) < (uint64_t)(2 * P - 1);
-        lds[lpos(e)] = (LT)v;
-    };
 
     {
         const GenTables& T = *Tp;
@@ -274,7 +254,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
             static_for<0, L - 1>([&](auto u) {
                 v[u] = gen_load((uint32_t)u < k ? ssrc + (uint64_t)u * BS : dsrc + (uint64_t)(u - k) * BS);
             });
-            static_for<0, L - 1>([&](auto u) { put((uint32_t)u * BS + tid, v[u]); });
+            static_for<0, L - 1>([&](auto u) { lds[lpos((uint32_t)u * BS + tid)] = v[u]; });
         } else {
             constexpr int U = 8;
             const uint64_t nb = B - b0 < (uint64_t)BS ? B - b0 : (uint64_t)BS;
@@ -290,7 +270,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                 });
                 static_for<0, U>([&](auto u) {
                     const uint32_t e = base + u * BS + tid;
-                    if (e < ns) put(e, e < valid ? v[u] : 0);
+                    if (e < ns) lds[lpos(e)] = e < valid ? v[u] : 0;
                 });
             }
             const uint32_t nd = (uint32_t)nb * t;
@@ -304,13 +284,9 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                 });
                 static_for<0, U>([&](auto u) {
                     const uint32_t e = base + u * BS + tid;
-                    if (e < nd) put(dbase + e, v[u]);
+                    if (e < nd) lds[lpos(dbase + e)] = v[u];
                 });
             }
-        }
-        if constexpr (N32) {
-            const bool wave_bad = __builtin_amdgcn_ballot_w64(!stage_ok) != 0;
-            if (lane == 0) wbad[tid >> 6] = wave_bad ? 1u : 0u;
         }
         __syncthreads();
 
@@ -319,35 +295,14 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         const bool live = b < B;
         int64_t raw[L];
         raw[0] = 0;
-        bool tile_bad = false;
-        if constexpr (N32) {
-            static_for<0, BS / 64>([&](auto w) { tile_bad = tile_bad || wbad[w] != 0; });
-        }
-        bool in_range = true;
-        if (!tile_bad) {
+        {
             const uint32_t es = lb * k - 1;                                    // + i,      i <= k
             const uint32_t ed = (uint32_t)BS * k + lb * t - 1 - k;             // + i,      i >  k
             // (lanes past B read whatever the LDS holds: they log nothing and store nothing)
             static_for<1, L>([&](auto i) { raw[i] = lds[lpos(((uint32_t)i <= k ? es : ed) + i)]; });
-            if constexpr (!N32)        // (N32: every staged value was checked on the way in)
-                static_for<1, L>([&](auto i) { in_range = in_range && ((uint64_t)(raw[i] + (P - 1)) < (uint64_t)(2 * P - 1)); });
-        } else {
-            // the tile holds an input outside (-p, p) (raw i64 secrets, rare): this lane's values from global
-            // memory, zero past D (batched.rs:37-43), and the range check per lane
-            static_for<1, L>([&](auto i) {
-                int64_t v = 0;
-                if (live) {
-                    if ((uint32_t)i <= k) {
-                        const uint64_t idx = b * k + (i - 1);
-                        v = idx < D ? sec[idx] : 0;
-                    } else {
-                        v = draws[((uint64_t)vec * B + b) * t + (i - 1 - k)];
-                    }
-                }
-                raw[i] = v;
-            });
-            static_for<1, L>([&](auto i) { in_range = in_range && ((uint64_t)(raw[i] + (P - 1)) < (uint64_t)(2 * P - 1)); });
         }
+        bool in_range = true;
+        static_for<1, L>([&](auto i) { in_range = in_range && ((uint64_t)(raw[i] + (P - 1)) < (uint64_t)(2 * P - 1)); });
         // A store pair (see the lane map above) takes the fast path only when both of its batches
         // are in range; otherwise both lanes log their batch for the generic exact fix-up kernel
         // (rare: raw i64 secrets) and the fast path below stores nothing for the pair.  (A call
