@@ -519,6 +519,7 @@ def main():
         rev_bytes = 8.0 * V * (len(idx) * B + Dm)
         side["shamir"] = {
             "config": "PackedShamir k=8 n=26 t=7 p=2147482801, 1M-dim, %d vectors/launch" % V,
+            "buffers": {"secrets": hex(sec.data_ptr()), "draws": hex(drw.data_ptr()), "shares": hex(sh.data_ptr())},
             "shares_per_s": V * n * B / (g_ms * 1e-3),
             "gen_ms": g_ms, "gen_GBps": gen_bytes / (g_ms * 1e-3) / 1e9,
             "gen_roofline_frac": gen_bytes / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,

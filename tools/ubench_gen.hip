@@ -49,6 +49,12 @@ __global__ __launch_bounds__(BS) void gen_mem(const int64_t* __restrict__ sec, c
         const uint32_t nl = (L % 8) * per + L / 8;
         if (nl >= total) return;
         L = nl;
+    } else if (remap >= 2) {   // XCD super-tiles of S = remap consecutive tiles, the 8 XCDs on adjacent super-tiles
+        const uint32_t S = (uint32_t)remap, total = gx * gridDim.y, round = total / (8 * S) * (8 * S);
+        if (L < round) {
+            const uint32_t x = L % 8, j = L / 8;
+            L = ((j / S) * 8 + x) * S + j % S;
+        }
     }
     const uint32_t vec = L / gx, tile = L % gx;
     const uint64_t b0 = (uint64_t)tile * BS;
@@ -260,11 +266,87 @@ static Res timeit(const char* name, double bytes, F launch, int reps) {
     return r;
 }
 
+// A share buffer of `bytes` built from physical chunks of `chunk` bytes (hipMemCreate), mapped into one
+// virtual range in order (shuffle = 0) or in a random order (shuffle = 1), so the buffer is physically
+// contiguous at most at the chunk's granularity.
+struct VmmBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    std::vector<hipMemGenericAllocationHandle_t> h;
+};
+static VmmBuf vmm_alloc(size_t bytes, size_t chunk, int shuffle) {
+    VmmBuf b;
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = 0;
+    size_t gran = 0;
+    CHECK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
+    chunk = (chunk + gran - 1) / gran * gran;
+    const size_t n = (bytes + chunk - 1) / chunk;
+    b.bytes = n * chunk;
+    CHECK(hipMemAddressReserve(&b.ptr, b.bytes, chunk, nullptr, 0));
+    b.h.resize(n);
+    for (size_t i = 0; i < n; ++i) CHECK(hipMemCreate(&b.h[i], chunk, &prop, 0));
+    std::vector<size_t> order(n);
+    for (size_t i = 0; i < n; ++i) order[i] = i;
+    if (shuffle) {
+        uint64_t s = 0x9e3779b97f4a7c15ull;
+        for (size_t i = n - 1; i > 0; --i) {
+            s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+            std::swap(order[i], order[s % (i + 1)]);
+        }
+    }
+    for (size_t i = 0; i < n; ++i) CHECK(hipMemMap((char*)b.ptr + i * chunk, chunk, 0, b.h[order[i]], 0));
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    CHECK(hipMemSetAccess(b.ptr, b.bytes, &acc, 1));
+    return b;
+}
+static void vmm_free(VmmBuf& b) {
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipMemUnmap(b.ptr, b.bytes));
+    for (auto& h : b.h) CHECK(hipMemRelease(h));
+    CHECK(hipMemAddressFree(b.ptr, b.bytes));
+}
+
 int main(int argc, char** argv) {
     const uint32_t V = argc > 1 ? (uint32_t)atoi(argv[1]) : 1000;
     const int reps = argc > 2 ? atoi(argv[2]) : 5;
     int64_t *sec, *dr, *out, *sink;
     const size_t sb = (size_t)V * D * 8, db = (size_t)V * B * T * 8, ob = (size_t)V * NR * B * 8;
+    if (argc > 3 && argv[3][0] == 'p') {     // placement mode: share-gen (XCD-chunked) into differently built share buffers
+        CHECK(hipMalloc(&sec, sb + 4096));
+        CHECK(hipMalloc(&dr, db + 4096));
+        CHECK(hipMemset(sec, 1, sb));
+        CHECK(hipMemset(dr, 2, db));
+        const double gen_bytes = (double)(sb + db + ob);
+        const dim3 grid((unsigned)((B + BS - 1) / BS), V), blk(BS);
+        printf("V = %u: share-gen memory model, XCD-chunked, %.3f GB per launch\n", V, gen_bytes / 1e9);
+        auto run = [&](const char* nm, int64_t* o) {
+            CHECK(hipMemset(o, 0, ob));
+            timeit(nm, gen_bytes, [&] { hipLaunchKernelGGL((gen_mem<0, 0, 0>), grid, blk, 0, 0, sec, dr, o, V, 1, 0); }, reps);
+        };
+        for (int i = 0; i < 3; ++i) {
+            CHECK(hipMalloc(&out, ob));
+            char nm[64];
+            snprintf(nm, sizeof nm, "hipMalloc share buffer %d", i);
+            run(nm, out);
+            CHECK(hipFree(out));
+        }
+        const size_t MB = 1 << 20;
+        for (size_t chunk : {2 * MB, 64 * MB, 1024 * MB}) {
+            for (int shuffle : {0, 1}) {
+                VmmBuf b = vmm_alloc(ob, chunk, shuffle);
+                char nm[64];
+                snprintf(nm, sizeof nm, "VMM %5zu MiB chunks, %s", chunk / MB, shuffle ? "shuffled" : "in order");
+                run(nm, (int64_t*)b.ptr);
+                vmm_free(b);
+            }
+        }
+        return 0;
+    }
     CHECK(hipMalloc(&sec, sb + 4096));
     CHECK(hipMalloc(&dr, db + 4096));
     CHECK(hipMalloc(&out, ob));
@@ -278,6 +360,16 @@ int main(int argc, char** argv) {
     const dim3 grid((unsigned)((B + BS - 1) / BS), V), blk(BS);
 #define GEN(LD, ST, POL, RM, ROT, NAME)                                                                         \
     timeit(NAME, gen_bytes, [&] { hipLaunchKernelGGL((gen_mem<LD, ST, POL>), grid, blk, 0, 0, sec, dr, out, V, RM, ROT); }, reps)
+    if (argc > 3) {     // quick mode: the XCD order variants only
+        GEN(0, 0, 0, 0, 0, "natural order");
+        GEN(0, 0, 0, 1, 0, "XCD-chunked (eighths of the grid)");
+        for (int S : {4, 16, 64, 256, 1024}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "XCD super-tiles of %d tiles", S);
+            timeit(nm, gen_bytes, [&] { hipLaunchKernelGGL((gen_mem<0, 0, 0>), grid, blk, 0, 0, sec, dr, out, V, S, 0); }, reps);
+        }
+        return 0;
+    }
     GEN(0, 0, 0, 0, 0, "today: ld8 -> LDS, permlane x4 nt");
     GEN(1, 0, 0, 0, 0, "ld16 -> LDS, permlane x4 nt");
     GEN(2, 0, 0, 0, 0, "LDS-DMA, permlane x4 nt");
