@@ -324,6 +324,16 @@ def main():
         if world > 1:
             dist.barrier()
 
+    # The side legs' resident buffers come from sda_hbm_alloc: one virtual range over fixed-size physical
+    # chunks, so share-gen's rate does not depend on how fragmented the box's free VRAM is (DESIGN.md "HBM
+    # backing", profiles/r04t, r04u).  SDA_BENCH_ALLOC=torch switches back to torch's allocator (A/B).
+    alloc_kind = "torch" if os.environ.get("SDA_BENCH_ALLOC", "hbm") == "torch" else "hbm"
+
+    def hbm(shape, dtype=torch.int64):
+        if alloc_kind == "torch":
+            return torch.empty(shape, dtype=dtype, device=dev)
+        return eng.hbm_empty(shape if isinstance(shape, tuple) else (shape,), dtype)
+
     if args.config == 4:
         run_config4(args, torch, dist, eng, dev, stream, barrier, world, rank, backend)
         if world > 1:
@@ -345,6 +355,8 @@ def main():
     side = {}
     if run_combine:
         R = tile if tile else N
+        # torch.empty (one hipMalloc) here: the combine ran 1.5 % faster on it than on sda_hbm_alloc's chunks
+        # (12.80 vs 12.98 ms, 4 interleaved rounds, profiles/r04w), the reverse of share-gen
         shares = torch.empty((R, D), dtype=torch.int64, device=dev)
         eng.synth_fill_dev(shares.data_ptr(), R, D, SEED_BASE + 1 + 1000 * rank, 0, m, stream())
         partial = torch.empty(D, dtype=torch.int64, device=dev)
@@ -479,14 +491,14 @@ def main():
         p, k, t, n = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count
         V, Dm = args.shamir_vectors, 1_000_000
         B = Dm // k
-        sec = torch.empty((V, Dm), dtype=torch.int64, device=dev)
+        sec = hbm((V, Dm))
         eng.synth_fill_dev(sec.data_ptr(), V, Dm, SEED_BASE + 2, 0, p, stream())
-        drw = torch.empty((V, B, t), dtype=torch.int64, device=dev)
+        drw = hbm((V, B, t))
         eng.synth_fill_dev(drw.data_ptr(), V * B, t, SEED_BASE + 22, 0, p - 1, stream())
-        sh = torch.empty((V, n, B), dtype=torch.int64, device=dev)
+        sh = hbm((V, n, B))
         idx = list(range(n - (t + k), n))           # a t+k clerk subset (result_ready threshold)
-        sub = torch.empty((V, len(idx), B), dtype=torch.int64, device=dev)
-        rev = torch.empty((V, Dm), dtype=torch.int64, device=dev)
+        sub = hbm((V, len(idx), B))
+        rev = hbm((V, Dm))
         gen_t, rex_t, rca_t, gca_t = Timer(torch), Timer(torch), Timer(torch), Timer(torch)
         # canonical-mode share-gen first (its shares are overwritten by the exact ones below)
         genc = lambda: eng.packed_generate_mode_dev(sch, sec.data_ptr(), Dm, V, drw.data_ptr(), sh.data_ptr(),  # noqa
@@ -519,7 +531,7 @@ def main():
         rev_bytes = 8.0 * V * (len(idx) * B + Dm)
         side["shamir"] = {
             "config": "PackedShamir k=8 n=26 t=7 p=2147482801, 1M-dim, %d vectors/launch" % V,
-            "buffers": {"secrets": hex(sec.data_ptr()), "draws": hex(drw.data_ptr()), "shares": hex(sh.data_ptr())},
+            "buffers": alloc_kind,
             "shares_per_s": V * n * B / (g_ms * 1e-3),
             "gen_ms": g_ms, "gen_GBps": gen_bytes / (g_ms * 1e-3) / 1e9,
             "gen_roofline_frac": gen_bytes / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
@@ -577,10 +589,11 @@ def main():
         # clerk payload path (clerk.rs:79-86 after the sealed-box opens): varint payloads of
         # signed field shares -> decode -> exact combine; plus the encode of the same matrix.
         Nc, Dc = args.codec_rows, 1_000_000
-        x = torch.empty((Nc, Dc), dtype=torch.int64, device=dev)
+        x = hbm((Nc, Dc))
         eng.synth_fill_dev(x.data_ptr(), Nc, Dc, SEED_BASE + 6, -(m - 1), m, stream())
         cap = Nc * Dc * 6 + 32                          # |v| < 2^31 -> zigzag < 2^32 -> <= 5 bytes
-        buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        buf = hbm(cap, torch.uint8)
+        buf.zero_()
         et, dt_, ct = Timer(torch), Timer(torch), Timer(torch)
         rb = None
         for i in range(3):
@@ -592,7 +605,7 @@ def main():
         rb = eng.varint_encode_dev(x.data_ptr(), Nc, Dc, Dc, buf.data_ptr(), cap, stream())
         off = np.concatenate([[0], np.cumsum(rb)]).astype(np.uint64)
         payload = float(off[-1])
-        mat = torch.empty((Nc, Dc), dtype=torch.int64, device=dev)
+        mat = hbm((Nc, Dc))
         cout = torch.empty(Dc, dtype=torch.int64, device=dev)
         for i in range(4):
             f = lambda: eng.varint_decode_dev(buf.data_ptr(), off, mat.data_ptr(), Dc, stream())  # noqa
@@ -667,10 +680,10 @@ def main():
         lens = g.integers(600_000, 635_000, size=Ps * ncl)
         poff = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
         total = int(poff[-1])
-        src = torch.empty(total + 32, dtype=torch.uint8, device=dev)
+        src = hbm(total + 32, torch.uint8)
         eng.synth_fill_dev(src.data_ptr(), 1, (total + 32) // 8, SEED_BASE + 11, -(2**61), 2**61, stream())
         need, _, _ = eng.snapshot_transpose_dev(src.data_ptr(), poff, Ps, ncl)
-        dst = torch.empty(need, dtype=torch.uint8, device=dev)
+        dst = hbm(need, torch.uint8)
         stt = Timer(torch)
         for i in range(2 + max(2, args.steps // 4)):
             f = lambda: eng.snapshot_transpose_dev(src.data_ptr(), poff, Ps, ncl, dst.data_ptr(), need, stream())  # noqa
@@ -784,7 +797,8 @@ def main():
                        **({"tile_rows": tile, "participations_total": 100_000} if tile else {}),
                        "parallelism": f"participation split x{world}" + ((", RCCL int64 all-reduce" if backend == "nccl" else f", {backend} int64 all-reduce (rehearsal)")
                                                                        if world > 1 else ""),
-                       "exact": "combiner.rs:16-28 recurrence, bit-exact"},
+                       "exact": "combiner.rs:16-28 recurrence, bit-exact",
+                       "buffers": "torch.empty"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic[0], "traffic_source": traffic[1]},

@@ -173,4 +173,8 @@ extern "C" {
     // ---- synthetic benchmark input ----
     pub fn sda_synth_fill_dev(h: *mut SdaEngine, dst: *mut i64, rows: u64, cols: u64, seed: u64, lo: i64, hi: i64,
                               stream: *mut c_void) -> SdaStatus;
+
+    // ---- HBM for resident buffers (fixed-size physical chunks) ----
+    pub fn sda_hbm_alloc(device: c_int, bytes: u64, out: *mut *mut c_void) -> SdaStatus;
+    pub fn sda_hbm_free(ptr: *mut c_void) -> SdaStatus;
 }

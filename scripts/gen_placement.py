@@ -2,7 +2,9 @@
 workload: canonical and exact share-gen into each of several freshly allocated share buffers (and from a
 second secrets/draws pair), mean of 8 launches each, two rounds.  Prints one line per (buffers, mode).
 
-    python scripts/gen_placement.py [n_share_buffers]
+    python scripts/gen_placement.py [n_share_buffers] [torch|hbm]
+
+hbm: every buffer from Engine.hbm_empty (sda_hbm_alloc, fixed-size physical chunks) instead of torch.empty.
 """
 import sys
 
@@ -17,6 +19,10 @@ def main():
     nbuf = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     eng = Engine(0)
     dev = torch.device("cuda", 0)
+    if len(sys.argv) > 2 and sys.argv[2] == "hbm":
+        empty = lambda shape: eng.hbm_empty(shape, torch.int64)  # noqa: E731
+    else:
+        empty = lambda shape: torch.empty(shape, dtype=torch.int64, device=dev)  # noqa: E731
     st = torch.cuda.current_stream().cuda_stream
     sch = S.CONFIG_PACKED
     p, k, t, n = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count
@@ -24,14 +30,14 @@ def main():
     B = Dm // k
 
     def inputs(seed):
-        sec = torch.empty((V, Dm), dtype=torch.int64, device=dev)
+        sec = empty((V, Dm))
         eng.synth_fill_dev(sec.data_ptr(), V, Dm, seed, 0, p, st)
-        drw = torch.empty((V, B, t), dtype=torch.int64, device=dev)
+        drw = empty((V, B, t))
         eng.synth_fill_dev(drw.data_ptr(), V * B, t, seed + 20, 0, p - 1, st)
         return sec, drw
 
     pairs = [inputs(0x5DA + 2)]
-    shs = [torch.empty((V, n, B), dtype=torch.int64, device=dev) for _ in range(nbuf)]
+    shs = [empty((V, n, B)) for _ in range(nbuf)]
     pairs.append(inputs(0x5DA + 3))
     torch.cuda.synchronize()
 

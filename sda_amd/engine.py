@@ -94,6 +94,8 @@ SIGNATURES = [
     ("sda_additive_generate_dev", _st, [_vp, C.c_int64, C.c_uint64, _vp, C.c_uint64, _vp, _vp, _vp]),
     ("sda_chacha_mask_combine_dev", _st, [_vp, C.c_int64, C.c_uint64, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
     ("sda_synth_fill_dev", _st, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int64, C.c_int64, _vp]),
+    ("sda_hbm_alloc", _st, [C.c_int, C.c_uint64, C.POINTER(_vp)]),
+    ("sda_hbm_free", _st, [_vp]),
     ("sda_varint_encode", _st, [_vp, _i64p, C.c_uint64, _u8p, C.c_uint64, _u64p]),
     ("sda_varint_decode", _st, [_vp, _u8p, C.c_uint64, _i64p, C.c_uint64, _u64p]),
     ("sda_clerk_decode_combine", _st, [_vp, C.POINTER(S.SharingSchemeC), C.POINTER(_u8p), _u64p, C.c_uint64,
@@ -162,6 +164,30 @@ def _rows(rows):
     ptrs = (_i64p * max(n, 1))(*[_ptr(a) for a in arrs])
     lens = (C.c_uint64 * max(n, 1))(*[a.size for a in arrs])
     return arrs, ptrs, lens, n
+
+
+class _HbmBlock:
+    """One sda_hbm_alloc buffer, exposed through __cuda_array_interface__ so torch.as_tensor wraps it
+    without a copy; torch keeps this object alive as long as the tensor, and its release frees the buffer."""
+
+    _TYPESTR = {"torch.int64": "<i8", "torch.int32": "<i4", "torch.uint8": "|u1", "torch.float64": "<f8",
+                "torch.float32": "<f4"}
+
+    def __init__(self, lib, device, shape, dtype, nbytes):
+        typestr = self._TYPESTR.get(str(dtype))
+        if typestr is None:
+            raise ValueError(f"hbm_empty: unsupported dtype {dtype}")
+        self.lib = lib
+        p = _vp()
+        _check(lib.sda_hbm_alloc(device, nbytes, C.byref(p)))
+        self.ptr = p.value
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (self.ptr, False),
+                                         "version": 2, "strides": None}
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self.lib.sda_hbm_free(self.ptr)
+            self.ptr = None
 
 
 class Engine:
@@ -306,6 +332,19 @@ class Engine:
 
     def synchronize(self):
         _check(self.lib.sda_engine_synchronize(self.h))
+
+    def hbm_empty(self, shape, dtype=None):
+        """An uninitialised torch tensor on this engine's device, in an sda_hbm_alloc buffer (fixed-size
+        physical chunks, DESIGN.md "HBM backing"); the buffer is released when the tensor is."""
+        import torch
+        dtype = dtype or torch.int64
+        shape = tuple(int(s) for s in shape)
+        count = 1
+        for s in shape:
+            count *= s
+        nbytes = max(count * torch.empty((), dtype=dtype).element_size(), 1)
+        return torch.as_tensor(_HbmBlock(self.lib, self.device, shape, dtype, nbytes),
+                               device=torch.device("cuda", self.device))
 
     # ---------------- device-resident entry points (raw device pointers, hipStream_t) ----------------
     def combine_dev(self, modulus, shares_ptr, n, dim, row_stride, out_ptr, stream=None):

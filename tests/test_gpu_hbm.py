@@ -1,0 +1,70 @@
+"""sda_hbm_alloc / sda_hbm_free (include/sda_engine.h) and Engine.hbm_empty on the GPU: the buffer is usable
+by torch and by the engine's kernels, share-gen into it is bit-identical to share-gen into a torch buffer, it
+is released with its tensor, and the error behaviour is the header's."""
+import ctypes as C
+
+import pytest
+
+from sda_amd import SdaError, schemes as S
+from sda_amd import engine as E
+
+pytestmark = pytest.mark.gpu
+
+
+def test_hbm_alloc_free_errors(engine):
+    lib = E.load_library()
+    p = C.c_void_p()
+    assert lib.sda_hbm_alloc(engine.device, 0, C.byref(p)) == E.ERR_INVALID_ARGUMENT
+    assert lib.sda_hbm_alloc(engine.device, 4096, None) == E.ERR_INVALID_ARGUMENT
+    assert lib.sda_hbm_free(None) == E.OK
+    assert lib.sda_hbm_alloc(engine.device, 5 << 20, C.byref(p)) == E.OK and p.value
+    assert lib.sda_hbm_free(C.c_void_p(p.value + 4096)) == E.ERR_INVALID_ARGUMENT   # not a returned pointer
+    assert lib.sda_hbm_free(p) == E.OK
+    assert lib.sda_hbm_free(p) == E.ERR_INVALID_ARGUMENT                          # already released
+    with pytest.raises(SdaError):
+        E._check(lib.sda_hbm_alloc(1 << 20, 4096, C.byref(p)))                    # no such device
+
+
+def test_hbm_tensor_torch_and_engine(engine):
+    import torch
+    st = torch.cuda.current_stream().cuda_stream
+    rows, cols = 300, 1 << 20                                  # 2.4 GB: many 64 MiB chunks
+    a = engine.hbm_empty((rows, cols))
+    assert a.is_cuda and a.dtype == torch.int64 and tuple(a.shape) == (rows, cols) and a.is_contiguous()
+    a.fill_(3)
+    assert int(a.sum()) == 3 * a.numel()
+    engine.synth_fill_dev(a.data_ptr(), rows, cols, 11, -5, 1000, st)
+    b = torch.empty_like(a)
+    engine.synth_fill_dev(b.data_ptr(), rows, cols, 11, -5, 1000, st)
+    assert torch.equal(a, b)
+    u8 = engine.hbm_empty((12345,), torch.uint8)
+    assert u8.dtype == torch.uint8 and u8.numel() == 12345
+    u8.zero_()
+    assert int(u8.sum()) == 0
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    del a
+    torch.cuda.synchronize()
+    assert torch.cuda.mem_get_info()[0] - free0 >= rows * cols * 8     # released with its tensor
+
+
+def test_packed_generate_into_hbm_matches_torch_buffer(engine):
+    import torch
+    st = torch.cuda.current_stream().cuda_stream
+    sch = S.CONFIG_PACKED
+    p, k, t, n = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count
+    V, Dm = 40, 1_000_000
+    B = Dm // k
+    sec = engine.hbm_empty((V, Dm))
+    engine.synth_fill_dev(sec.data_ptr(), V, Dm, 21, 0, p, st)
+    drw = engine.hbm_empty((V, B, t))
+    engine.synth_fill_dev(drw.data_ptr(), V * B, t, 22, 0, p - 1, st)
+    for mode in (E.REVEAL_EXACT, E.REVEAL_CANONICAL):
+        sh_h = engine.hbm_empty((V, n, B))
+        sh_t = torch.empty((V, n, B), dtype=torch.int64, device=sec.device)
+        for sh in (sh_h, sh_t):
+            engine.packed_generate_mode_dev(sch, sec.data_ptr(), Dm, V, drw.data_ptr(), sh.data_ptr(), mode, st)
+        torch.cuda.synchronize()
+        assert torch.equal(sh_h, sh_t)
+        if mode == E.REVEAL_CANONICAL:
+            assert int(sh_h.min()) >= 0 and int(sh_h.max()) < p
