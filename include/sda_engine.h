@@ -338,9 +338,11 @@ sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64
 /* HBM for the resident hot-path buffers (no reference counterpart: the reference's buffers are Rust
  * Vec<i64> on the host, batched.rs:25-28).  `bytes` of device memory on `device`, one virtual range
  * mapped from physical chunks of SDA_HBM_CHUNK_MB (default 64) MiB, so its backing never depends on how
- * fragmented the driver's free VRAM is (DESIGN.md "HBM backing").  The range is rounded up to whole chunks.
- * sda_hbm_free waits for the device, then unmaps and releases the buffer; NULL is a no-op, any pointer
- * not returned by sda_hbm_alloc is INVALID_ARGUMENT. */
+ * fragmented the driver's free VRAM is.  The range is rounded up to whole chunks.
+ * sda_hbm_free waits for the device, then returns the buffer to a per-process pool: it stays mapped and a
+ * later sda_hbm_alloc of up to its size (and at least half of it) gets it back; the memory is released when
+ * the process ends.  NULL is a no-op; a pointer not returned by sda_hbm_alloc, or freed twice, is
+ * INVALID_ARGUMENT. */
 sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out);
 sda_status sda_hbm_free(void* ptr);
 

@@ -865,6 +865,11 @@ sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64
 // chunks of a fixed size (hipMemCreate, SDA_HBM_CHUNK_MB, default 64 MiB) ran at the fast rate in every
 // case measured, whatever the chunk size (2 MiB - 1 GiB) and whether the chunks were mapped in order or
 // shuffled (profiles/r04r).  sda_hbm_alloc / sda_hbm_free give the resident hot-path buffers that backing.
+//
+// A freed buffer stays mapped, in a per-process pool that later allocations reuse (best fit, at most twice
+// the size asked for).  Unmapping and releasing a buffer, then letting the runtime hand its virtual range to
+// other allocations, corrupted data in the GPU suite (profiles/r04y: reads of a torch temporary returned a
+// different count each time), so no range is ever unmapped while the process runs.
 namespace {
 
 struct HbmBuffer {
@@ -873,7 +878,8 @@ struct HbmBuffer {
     std::vector<hipMemGenericAllocationHandle_t> chunks;
 };
 std::mutex g_hbm_mu;
-std::map<uintptr_t, HbmBuffer> g_hbm;
+std::map<uintptr_t, HbmBuffer> g_hbm;                   // handed out
+std::map<uintptr_t, HbmBuffer> g_hbm_pool;              // freed, still mapped
 
 size_t hbm_chunk_bytes() {
     const char* e = getenv("SDA_HBM_CHUNK_MB");
@@ -881,7 +887,7 @@ size_t hbm_chunk_bytes() {
     return (size_t)(mb > 0 ? mb : 64) << 20;
 }
 
-// unmap and release everything a (possibly partly built) buffer holds
+// unmap and release what a partly built buffer holds (the failure path of sda_hbm_alloc only)
 void hbm_release(void* ptr, HbmBuffer& b, size_t mapped_chunks, size_t chunk) {
     for (size_t i = 0; i < mapped_chunks; ++i) (void)hipMemUnmap(static_cast<char*>(ptr) + i * chunk, chunk);
     for (auto& c : b.chunks) (void)hipMemRelease(c);
@@ -907,6 +913,22 @@ sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out) {
     if (gran == 0) gran = 4096;
     const size_t chunk = (hbm_chunk_bytes() + gran - 1) / gran * gran;
     const size_t n = (size_t)((bytes + chunk - 1) / chunk);
+    {   // a pooled buffer of this device that fits, the smallest one (at most twice the size)
+        std::lock_guard<std::mutex> lk(g_hbm_mu);
+        auto best = g_hbm_pool.end();
+        for (auto it = g_hbm_pool.begin(); it != g_hbm_pool.end(); ++it) {
+            const HbmBuffer& c = it->second;
+            if (c.device == device && c.bytes >= bytes && c.bytes <= 2 * n * chunk &&
+                (best == g_hbm_pool.end() || c.bytes < best->second.bytes))
+                best = it;
+        }
+        if (best != g_hbm_pool.end()) {
+            *out = reinterpret_cast<void*>(best->first);
+            g_hbm[best->first] = std::move(best->second);
+            g_hbm_pool.erase(best);
+            return ok();
+        }
+    }
     HbmBuffer b;
     b.device = device;
     b.bytes = n * chunk;
@@ -947,18 +969,21 @@ sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out) {
 sda_status sda_hbm_free(void* ptr) {
     SDA_ENTRY;
     if (!ptr) return ok();
-    HbmBuffer b;
+    int device = 0;
     {
         std::lock_guard<std::mutex> lk(g_hbm_mu);
         auto it = g_hbm.find(reinterpret_cast<uintptr_t>(ptr));
         if (it == g_hbm.end()) return fail(SDA_ERR_INVALID_ARGUMENT, "%p was not returned by sda_hbm_alloc", ptr);
-        b = std::move(it->second);
-        g_hbm.erase(it);
+        device = it->second.device;
     }
-    HIP_TRY(hipSetDevice(b.device));
-    HIP_TRY(hipDeviceSynchronize());      // work queued on any stream may still use the buffer
-    const size_t chunk = b.chunks.empty() ? 0 : b.bytes / b.chunks.size();
-    hbm_release(ptr, b, b.chunks.size(), chunk);
+    // work queued on any stream may still use the buffer: it returns to the pool once the device is idle
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipDeviceSynchronize());
+    std::lock_guard<std::mutex> lk(g_hbm_mu);
+    auto it = g_hbm.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == g_hbm.end()) return fail(SDA_ERR_INVALID_ARGUMENT, "%p was freed twice", ptr);
+    g_hbm_pool[it->first] = std::move(it->second);
+    g_hbm.erase(it);
     return ok();
 }
 
