@@ -1,0 +1,45 @@
+#!/bin/bash
+# Copy one gpu_final.sh session (gpurun_out/<tag>/, gpurun_out/pmc_<tag>_{shamir,chacha}/) into profiles/<tag>/,
+# in the layout profiles/README.md describes, then point profiles/combine_traffic.json at its combine passes
+# and regenerate profiles/valu_roofline.json from its trace and SQ passes.
+#   bash scripts/save_evidence.sh <tag>
+set -euo pipefail
+cd "$(dirname "$0")/.."
+TAG=$1
+S=gpurun_out/$TAG
+D=profiles/$TAG
+mkdir -p "$D/configs"
+cp "$S/bench_4.json" "$D/bench.json"
+cp "$S/bench_4.log" "$D/bench.log"
+cp "$S/bench_traced.json" "$D/bench_traced.json"
+cp "$S/host.txt" "$S/smoke.log" "$S/kernel_stats_by_grid.csv" "$S/pmc_6.txt" "$S/pmc_7.txt" "$D/"
+cp "$S/trace/run_kernel_stats.csv" "$D/kernel_stats.csv"
+tail -2 "$S/pytest_2.log" > "$D/pytest_gpu_summary.txt"
+cp "$S/sh_8.txt" "$D/pmc_shamir.txt"
+cp "$S/sh_9.txt" "$D/pmc_chacha.txt"
+cp "$S/bench_10.json" "$D/configs/config3.json"
+cp "$S/bench_10.log" "$D/configs/config3.log"
+cp "$S/bench_11.json" "$D/configs/config4.json"
+cp "$S/bench_11.log" "$D/configs/config4.log"
+python3 - "$TAG" <<'EOF'
+import json, re, sys
+tag = sys.argv[1]
+def kib(path, ctr):
+    txt = open(f"profiles/{tag}/{path}").read()
+    m = re.search(r"combine_exact_kernel<long, 2, 8, true, false, false>\n\s+" + ctr + r"\s+([0-9.e+]+)", txt)
+    return float(m.group(1))
+fetch, write = kib("pmc_6.txt", "FETCH_SIZE"), kib("pmc_7.txt", "WRITE_SIZE")
+traffic = int(round((2 * fetch + write) * 1024))
+p = "profiles/combine_traffic.json"
+d = json.load(open(p))
+for l in d["launches"]:
+    if l["rows"] == 10000 and l["dim"] == 1000000:
+        l["hbm_bytes_per_launch"] = traffic
+        l["source"] = f"profiles/{tag}/pmc_6.txt + pmc_7.txt (2 x FETCH_SIZE + WRITE_SIZE, KiB)"
+json.dump(d, open(p, "w"), indent=1)
+print("combine traffic per launch:", traffic, "B =", traffic / (8 * (10000 * 1000000 + 1000000)), "x algorithmic")
+EOF
+python3 scripts/kernel_report.py "$S/trace" "gpurun_out/pmc_${TAG}_shamir" "gpurun_out/pmc_${TAG}_chacha" \
+  > "$D/kernel_report.json"
+python3 scripts/valu_mix.py profiles/r02b/ubench_int.txt "$D/kernel_report.json" > profiles/valu_roofline.json
+echo "saved $D"
