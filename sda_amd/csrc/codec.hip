@@ -229,8 +229,9 @@ __global__ __launch_bounds__(kThreads) void varint_count_kernel(const uint8_t* _
 __global__ __launch_bounds__(kThreads) void varint_scan_kernel(const uint32_t* __restrict__ region_count,
                                                                const uint64_t* __restrict__ blob_region,
                                                                uint64_t* __restrict__ region_base,
-                                                               uint64_t* __restrict__ blob_count) {
-    const uint32_t b = blockIdx.x;
+                                                               uint64_t* __restrict__ blob_count,
+                                                               uint32_t b0 = 0) {
+    const uint32_t b = b0 + blockIdx.x;
     const uint64_t r0 = blob_region[b], r1 = blob_region[b + 1];
     __shared__ uint64_t part[kThreads];
     uint64_t carry = 0;
@@ -459,10 +460,11 @@ __global__ __launch_bounds__(kThreads) void varint_cap_kernel(const uint64_t* __
     if (over) atomicOr(flag, 1u);
 }
 
-__global__ __launch_bounds__(kThreads) void slot_dims_kernel(const uint64_t* __restrict__ blob_count, uint64_t n_blobs,
-                                                             uint32_t* __restrict__ flags) {
+// blobs [b0, b1) against blob 0's count
+__global__ __launch_bounds__(kThreads) void slot_dims_kernel(const uint64_t* __restrict__ blob_count, uint64_t b1,
+                                                             uint32_t* __restrict__ flags, uint64_t b0 = 0) {
     bool bad = false;
-    for (uint64_t b = threadIdx.x; b < n_blobs; b += kThreads) bad |= blob_count[b] != blob_count[0];
+    for (uint64_t b = b0 + threadIdx.x; b < b1; b += kThreads) bad |= blob_count[b] != blob_count[0];
     if (bad) atomicOr(flags, 2u);
 }
 
@@ -471,9 +473,12 @@ __global__ __launch_bounds__(kThreads) void slot_plan_kernel(const uint64_t* __r
                                                              const uint32_t* __restrict__ region_count, uint32_t y0,
                                                              uint64_t n_blobs, uint64_t ntiles, uint32_t tile,
                                                              const uint32_t* __restrict__ flags,
-                                                             uint64_t* __restrict__ plan) {
+                                                             uint64_t* __restrict__ plan, uint64_t pb0 = 0,
+                                                             uint64_t rbase = 0) {
+    // grouped job (pb0, rbase > 0): blob b of the group [pb0, pb0 + n_blobs) is plan column b - pb0, and its
+    // region r sits at slot (r - rbase) * kSlotCap of the group's slot buffer
     if (*flags) return;
-    const uint64_t b = y0 + blockIdx.y;
+    const uint64_t b = pb0 + y0 + blockIdx.y;
     const uint64_t r0 = blob_region[b], r1 = blob_region[b + 1];
     const uint64_t r = r0 + (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (r >= r1) return;
@@ -483,7 +488,7 @@ __global__ __launch_bounds__(kThreads) void slot_plan_kernel(const uint64_t* __r
     for (uint64_t t = (E0 + tile - 1) / tile; t < ntiles && t * tile < E1; ++t) {
         const uint64_t local = t * tile - E0;
         const uint64_t c0 = E1 - t * tile < tile ? E1 - t * tile : tile;
-        plan[t * n_blobs + b] = slot_plan_entry(r * kSlotCap + local, c0, gap);
+        plan[t * n_blobs + (b - pb0)] = slot_plan_entry((r - rbase) * kSlotCap + local, c0, gap);
     }
 }
 
@@ -500,7 +505,8 @@ __global__ __launch_bounds__(kThreads) void slot_combine_kernel(const int32_t* _
                                                                 const uint64_t* __restrict__ plan,
                                                                 uint64_t n_blobs, const uint64_t* __restrict__ dim_p,
                                                                 const uint32_t* __restrict__ flags, uint64_t out_cap,
-                                                                int64_t* __restrict__ out, Mod64 M) {
+                                                                int64_t* __restrict__ out, Mod64 M,
+                                                                const int64_t* __restrict__ acc_in = nullptr) {
     typedef typename std::conditional<CPL == 1, int32_t,
             int32_t __attribute__((ext_vector_type(CPL == 1 ? 2 : CPL)))>::type V;
     constexpr uint32_t kTile = CPL * kThreads;
@@ -529,9 +535,9 @@ __global__ __launch_bounds__(kThreads) void slot_combine_kernel(const int32_t* _
         }
         return v;
     };
-    int64_t acc[CPL];
+    int64_t acc[CPL];     // the recurrence's state: 0, or where the previous group of blobs left it
 #pragma unroll
-    for (int i = 0; i < CPL; ++i) acc[i] = 0;
+    for (int i = 0; i < CPL; ++i) acc[i] = (acc_in && e0 + o + i < dim) ? acc_in[e0 + o + i] : 0;
     uint64_t b = 0;
     for (; b + UNROLL <= n_blobs; b += UNROLL) {
         V v[UNROLL];
@@ -550,6 +556,17 @@ __global__ __launch_bounds__(kThreads) void slot_combine_kernel(const int32_t* _
 #pragma unroll
     for (int i = 0; i < CPL; ++i)
         if (e0 + o + i < dim) out[e0 + o + i] = acc[i];
+}
+
+// grouped slot path: the finished state goes to out only when no flag is set and the dimension fits
+__global__ __launch_bounds__(kThreads) void slot_commit_kernel(const int64_t* __restrict__ acc,
+                                                               const uint64_t* __restrict__ dim_p,
+                                                               const uint32_t* __restrict__ flags, uint64_t out_cap,
+                                                               int64_t* __restrict__ out) {
+    const uint64_t dim = *dim_p;
+    if (*flags || dim > out_cap) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < dim; i += (uint64_t)gridDim.x * kThreads)
+        out[i] = acc[i];
 }
 
 // ---------------- the clerk's fused decode -> combine ----------------
@@ -1212,9 +1229,34 @@ static uint32_t slot_cpl() {
     return (v == 1 || v == 2) ? (uint32_t)v : 4u;
 }
 
+// Blobs per group of the slot path (SDA_CODEC_GROUP; 0 = the whole job in one pass).  Grouped, each group
+// is decoded into one reused slot buffer and combined from it at once, while its slots may still sit in the
+// caches, the recurrence's state carried from group to group in a scratch row.
+static uint64_t slot_group() {
+    const char* e = getenv("SDA_CODEC_GROUP");
+    return e ? strtoull(e, nullptr, 10) : 0;
+}
+struct SlotGroups {
+    uint64_t G;            // blobs per group (0: one pass)
+    uint64_t regions;      // slot regions of the largest group (all regions in one pass)
+};
+static SlotGroups slot_groups(const VarintPlan& plan, uint64_t n_blobs) {
+    const uint64_t G = std::min<uint64_t>(slot_group(), 65535);     // grid.y of a group's launches
+    if (G == 0 || G >= n_blobs) return {0, plan.regions};
+    uint64_t mx = 0;
+    for (uint64_t g0 = 0; g0 < n_blobs; g0 += G) {
+        const uint64_t g1 = g0 + G < n_blobs ? g0 + G : n_blobs;
+        mx = std::max<uint64_t>(mx, plan.blob_region[g1] - plan.blob_region[g0]);
+    }
+    return {G, mx};
+}
+// slot buffer layout: [slots | tile plan | (grouped) the recurrence's state, dim i64]
+static size_t slot_area_bytes(uint64_t regions) { return (regions * kSlotCap + (kRegionBytes - kSlotCap)) * sizeof(int32_t); }
+
 size_t varint_slot_bytes(const VarintPlan& plan, uint64_t n_blobs, uint64_t dim) {
     const uint64_t ntiles = (dim + kThreads - 1) / kThreads;          // plan room for the smallest tile
-    return (plan.regions * kSlotCap + (kRegionBytes - kSlotCap)) * sizeof(int32_t) + ntiles * n_blobs * 8 + 256;
+    const SlotGroups sg = slot_groups(plan, n_blobs);
+    return slot_area_bytes(sg.regions) + ntiles * (sg.G ? sg.G : n_blobs) * 8 + (sg.G ? dim * 8 : 0) + 256;
 }
 
 hipError_t launch_varint_decode_slots_combine(const uint8_t* bytes, const uint64_t* blob_off_host, uint64_t n_blobs,
@@ -1223,9 +1265,9 @@ hipError_t launch_varint_decode_slots_combine(const uint8_t* bytes, const uint64
                                               uint32_t* flags_host, hipStream_t s) {
     const size_t R = plan.regions;
     DecodeWork w = carve(work, R, n_blobs);
+    const SlotGroups sg = slot_groups(plan, n_blobs);
     int32_t* slots = static_cast<int32_t*>(slot_buf);
-    uint64_t* tplan = reinterpret_cast<uint64_t*>(static_cast<char*>(slot_buf) +
-                                                  (R * kSlotCap + (kRegionBytes - kSlotCap)) * sizeof(int32_t));
+    uint64_t* tplan = reinterpret_cast<uint64_t*>(static_cast<char*>(slot_buf) + slot_area_bytes(sg.regions));
     const uint32_t cpl = slot_cpl(), tile = cpl * kThreads;
     // the grid's bound: blob 0 decodes to at most one element per byte
     const uint64_t ntiles = (blob_off_host[1] - blob_off_host[0] + tile - 1) / tile;
@@ -1234,6 +1276,57 @@ hipError_t launch_varint_decode_slots_combine(const uint8_t* bytes, const uint64
     if ((e = hipMemcpyAsync(w.blob_off, blob_off_host, (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     if ((e = hipMemcpyAsync(w.blob_region, plan.blob_region.data(), (n_blobs + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.wide, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+    const Mod64 M = make_mod64(modulus > 0 ? modulus : 1);
+    const bool small_m = modulus <= ((int64_t)1 << 62);
+#define SLOT_COMBINE(C, SM, NB, DST, ACC_IN)                                                                       \
+    hipLaunchKernelGGL((slot_combine_kernel<C, 8, SM>), dim3((unsigned)ntiles), dim3(kThreads), 0, s, slots,         \
+                       (const uint64_t*)tplan, NB, (const uint64_t*)w.blob_count, (const uint32_t*)w.wide, out_cap, \
+                       DST, M, ACC_IN)
+#define SLOT_COMBINE_ANY(NB, DST, ACC_IN)                                                                            \
+    do {                                                                                                             \
+        if (cpl == 4) { if (small_m) SLOT_COMBINE(4, true, NB, DST, ACC_IN); else SLOT_COMBINE(4, false, NB, DST, ACC_IN); } \
+        else if (cpl == 2) { if (small_m) SLOT_COMBINE(2, true, NB, DST, ACC_IN); else SLOT_COMBINE(2, false, NB, DST, ACC_IN); } \
+        else { if (small_m) SLOT_COMBINE(1, true, NB, DST, ACC_IN); else SLOT_COMBINE(1, false, NB, DST, ACC_IN); } \
+    } while (0)
+    if (sg.G) {
+        // grouped: decode, scan, check and combine one group of blobs at a time through the one slot buffer
+        // (region r of the group starting at blob g0 sits at slot (r - blob_region[g0]) * kSlotCap); the
+        // state carried between groups lives in `acc`, and reaches out only if the whole job is clean
+        int64_t* acc = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(tplan) + ntiles * sg.G * 8);
+        for (uint64_t g0 = 0; g0 < n_blobs; g0 += sg.G) {
+            const uint64_t g1 = g0 + sg.G < n_blobs ? g0 + sg.G : n_blobs;
+            const uint64_t ng = g1 - g0, R0 = plan.blob_region[g0];
+            if (plan.blob_region[g1] > R0) {
+                hipLaunchKernelGGL((varint_decode_kernel<int32_t, true>), dim3((unsigned)plan.max_regions, (unsigned)ng),
+                                   dim3(kThreads), 0, s, bytes, w.blob_region, w.blob_off, (uint32_t)g0,
+                                   (const uint64_t*)nullptr, (const uint32_t*)nullptr, slots - R0 * kSlotCap, 0, w.wide,
+                                   w.region_count);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(varint_scan_kernel, dim3((unsigned)ng), dim3(kThreads), 0, s, w.region_count,
+                               w.blob_region, w.region_base, w.blob_count, (uint32_t)g0);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            hipLaunchKernelGGL(slot_dims_kernel, dim3(1), dim3(kThreads), 0, s, (const uint64_t*)w.blob_count, g1,
+                               w.wide, g0);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if (ntiles && modulus > 0) {
+                hipLaunchKernelGGL(slot_plan_kernel, dim3((unsigned)((plan.max_regions + kThreads - 1) / kThreads),
+                                   (unsigned)ng), dim3(kThreads), 0, s, w.blob_region, w.region_base, w.region_count,
+                                   0u, ng, ntiles, tile, (const uint32_t*)w.wide, tplan, g0, R0);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+                SLOT_COMBINE_ANY(ng, acc, g0 ? (const int64_t*)acc : (const int64_t*)nullptr);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+            }
+        }
+        if (ntiles && modulus > 0) {
+            hipLaunchKernelGGL(slot_commit_kernel, dim3(2048), dim3(kThreads), 0, s, (const int64_t*)acc,
+                               (const uint64_t*)w.blob_count, (const uint32_t*)w.wide, out_cap, out);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        if ((e = hipMemcpyAsync(counts_host, w.blob_count, n_blobs * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(flags_host, w.wide, sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        return hipStreamSynchronize(s);
+    }
     for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
         const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
         hipLaunchKernelGGL((varint_decode_kernel<int32_t, true>), dim3((unsigned)plan.max_regions, ny), dim3(kThreads),
@@ -1254,18 +1347,11 @@ hipError_t launch_varint_decode_slots_combine(const uint8_t* bytes, const uint64
                                n_blobs, ntiles, tile, (const uint32_t*)w.wide, tplan);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
-        const Mod64 M = make_mod64(modulus);
-        const bool small_m = modulus <= ((int64_t)1 << 62);
-        const dim3 g((unsigned)ntiles), blk(kThreads);
-#define SLOT_LAUNCH(C, SM)                                                                                 \
-    hipLaunchKernelGGL((slot_combine_kernel<C, 8, SM>), g, blk, 0, s, slots, (const uint64_t*)tplan, n_blobs, \
-                       (const uint64_t*)w.blob_count, (const uint32_t*)w.wide, out_cap, out, M)
-        if (cpl == 4) { if (small_m) SLOT_LAUNCH(4, true); else SLOT_LAUNCH(4, false); }
-        else if (cpl == 2) { if (small_m) SLOT_LAUNCH(2, true); else SLOT_LAUNCH(2, false); }
-        else { if (small_m) SLOT_LAUNCH(1, true); else SLOT_LAUNCH(1, false); }
-#undef SLOT_LAUNCH
+        SLOT_COMBINE_ANY(n_blobs, out, (const int64_t*)nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+#undef SLOT_COMBINE_ANY
+#undef SLOT_COMBINE
     // the call's one wait: the counts and the flags, after the whole job
     if ((e = hipMemcpyAsync(counts_host, w.blob_count, n_blobs * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipMemcpyAsync(flags_host, w.wide, sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;

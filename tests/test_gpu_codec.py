@@ -312,3 +312,45 @@ def test_decode_dev_capacity_leaves_output(engine, oracle, irregular):
     got = out.cpu().numpy()
     for i, e in enumerate(exp):
         assert_same(got[i, :e.size], e)
+
+
+@pytest.mark.parametrize("group", ["1", "3", "7", "64"])
+def test_grouped_slot_path(engine, oracle, monkeypatch, group):
+    """SDA_CODEC_GROUP: the slot path decoded and combined a group of blobs at a time, the recurrence's state
+    carried between groups.  Results equal combiner.rs:16-28's for signed shares; a blob of another length
+    in the LAST group, a short out_cap and a wide element (matrix fall-back) behave as the one-pass path
+    (error, out untouched / the exact result)."""
+    monkeypatch.setenv("SDA_CODEC_PATH", "slots")
+    monkeypatch.setenv("SDA_CODEC_GROUP", group)
+    m = 2147482801
+    rng = np.random.default_rng(91)
+    N, D = 23, 20_011
+    x = rng.integers(-(m - 1), m, size=(N, D), dtype=np.int64)
+    x[::4, :50] = rng.integers(-64, 64, size=(len(range(0, N, 4)), 50))     # short elements too
+    blobs = [oracle.varint_encode(r) for r in x]
+    t, off = _pack(blobs)
+    out = torch.full((D,), 7, dtype=torch.int64, device="cuda")
+    assert engine.clerk_decode_combine_dev(m, t.data_ptr(), off, out.data_ptr(), D) == D
+    torch.cuda.synchronize()
+    assert_same(out.cpu().numpy(), oracle.combine(m, x), f"group {group}")
+    # the last blob one element short: Wrong dimension, out untouched
+    bad = blobs[:-1] + [oracle.varint_encode(x[-1][:-1])]
+    tb, offb = _pack(bad)
+    out.fill_(7)
+    with pytest.raises(SdaError) as ei:
+        engine.clerk_decode_combine_dev(m, tb.data_ptr(), offb, out.data_ptr(), D)
+    assert ei.value.status == E.ERR_WRONG_DIMENSION
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy() == 7).all()
+    with pytest.raises(SdaError) as ei:
+        engine.clerk_decode_combine_dev(m, t.data_ptr(), off, out.data_ptr(), D - 1)
+    assert ei.value.status == E.ERR_INVALID_ARGUMENT
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy() == 7).all()
+    # a value past int32 in the last blob: the job takes the matrix path, still exact
+    y = x.copy()
+    y[-1, D // 2] = 2**40
+    ty, offy = _pack([oracle.varint_encode(r) for r in y])
+    assert engine.clerk_decode_combine_dev(m, ty.data_ptr(), offy, out.data_ptr(), D) == D
+    torch.cuda.synchronize()
+    assert_same(out.cpu().numpy(), oracle.combine(m, y), f"group {group} wide")
