@@ -898,11 +898,19 @@ void hbm_release(void* ptr, HbmBuffer& b, size_t mapped_chunks, size_t chunk) {
 
 extern "C" {
 
+// The caller's current device is left as it was (the HBM calls take a device, not a handle).
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() { if (hipGetDevice(&prev) != hipSuccess) prev = -1; }
+    ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
 sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out) {
     SDA_ENTRY;
     if (!out) return fail(SDA_ERR_INVALID_ARGUMENT, "out is NULL");
     *out = nullptr;
     if (bytes == 0) return fail(SDA_ERR_INVALID_ARGUMENT, "bytes must be > 0");
+    DeviceGuard dg;
     HIP_TRY(hipSetDevice(device));
     hipMemAllocationProp prop = {};
     prop.type = hipMemAllocationTypePinned;
@@ -977,6 +985,7 @@ sda_status sda_hbm_free(void* ptr) {
         device = it->second.device;
     }
     // work queued on any stream may still use the buffer: it returns to the pool once the device is idle
+    DeviceGuard dg;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipDeviceSynchronize());
     std::lock_guard<std::mutex> lk(g_hbm_mu);
