@@ -950,9 +950,14 @@ def valu_roofline(key, ms, waves, blocks=None):
     else:
         return None
     achieved = insts * 64 / (ms * 1e-3) / 1e12
-    return {"bound": "valu", "achieved": round(achieved, 3), "peak": k["mix_ceiling_T_lane_ops"],
-            "unit": "T lane-ops/s", "frac": round(achieved / k["mix_ceiling_T_lane_ops"], 4),
-            "valu_insts_per_launch": insts, "source": src}
+    r = {"bound": "valu", "achieved": round(achieved, 3), "peak": k["mix_ceiling_T_lane_ops"],
+         "unit": "T lane-ops/s", "frac": round(achieved / k["mix_ceiling_T_lane_ops"], 4),
+         "valu_insts_per_launch": insts, "source": src}
+    if k.get("pattern_ceiling_T_lane_ops"):      # the kernel's dependent pattern timed alone (tools/ubench_bank)
+        r["pattern_peak"] = k["pattern_ceiling_T_lane_ops"]
+        r["pattern_frac"] = round(achieved / k["pattern_ceiling_T_lane_ops"], 4)
+        r["pattern_source"] = k.get("pattern_source")
+    return r
 
 
 def traffic_from_profile(N, D):

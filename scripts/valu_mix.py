@@ -111,6 +111,22 @@ def disasm(src, define, frag):
     raise SystemExit(f"kernel {frag} not found in {src}")
 
 
+# ChaCha's quarter-round chains (4 per wave, add -> xor -> v_alignbit, the combine's 6 waves per SIMD) timed in
+# isolation by tools/ubench_bank: the rate the combine's own instruction stream can issue at, which the
+# independent per-class prices above overestimate (the QR pattern runs at 38.7 T, its mix prices at 52 T).
+PATTERN = {"chacha_combine": ("profiles/r04bank/ubench_bank.txt", "QR chains, different-bank pairs    6 waves/SIMD")}
+
+
+def pattern_ceiling(path, label):
+    try:
+        for line in open(os.path.join(ROOT, path)):
+            if line.startswith(label):
+                return float(line.split()[-3])
+    except OSError:
+        return None
+    return None
+
+
 def main():
     R = rates(sys.argv[1])
     report, sources = {}, {}
@@ -138,6 +154,12 @@ def main():
             rec["pmc_source"] = sources[hit]
             if key in PMC_BLOCKS:      # work units of the counted launch, to scale to other launch sizes
                 rec["pmc_blocks"] = PMC_BLOCKS[key]
+        if key in PATTERN:        # the kernel's dependent instruction pattern, measured on its own
+            path, label = PATTERN[key]
+            pc = pattern_ceiling(path, label)
+            if pc:
+                rec["pattern_ceiling_T_lane_ops"] = pc
+                rec["pattern_source"] = f"{path}: {label}"
         out["kernels"][key] = rec
     json.dump(out, sys.stdout, indent=1)
 
