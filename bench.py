@@ -370,10 +370,16 @@ def main():
         # N > 1: each step's sign flags come back asynchronously (SplitTicket); a step finishes the
         # PREVIOUS step's ticket after queueing its own work, so no host read sits between a step's
         # all-reduce and its finalize, and the GPU never waits for the host
+        # (two `out` buffers, alternating: a ticket in flight never shares its `out` with the next step's)
         pending = []
+        outs = [out, torch.empty(D, dtype=torch.int64, device=dev)]
+        nstep = [0]
 
         def step(timed):
+            nonlocal out
             teng.timing = timed
+            out = outs[nstep[0] % 2]
+            nstep[0] += 1
             if tile:
                 t = Dd.combine_tiles_sharded(teng, m, tiles, D, D, partial, out, defer=True)
             else:

@@ -66,6 +66,8 @@ extern "C" {
     pub fn sda_engine_create(device_ordinal: c_int, out: *mut *mut SdaEngine) -> SdaStatus;
     pub fn sda_engine_destroy(h: *mut SdaEngine);
     pub fn sda_engine_synchronize(h: *mut SdaEngine) -> SdaStatus;
+    pub fn sda_engine_create_multi(ordinals: *const c_int, n_devices: c_int, out: *mut *mut SdaEngine) -> SdaStatus;
+    pub fn sda_engine_device_count(h: *const SdaEngine) -> c_int;
     pub fn sda_last_error_message() -> *const c_char;
     pub fn sda_status_string(status: c_int) -> *const c_char;
 
@@ -177,4 +179,7 @@ extern "C" {
     // ---- HBM for resident buffers (fixed-size physical chunks) ----
     pub fn sda_hbm_alloc(device: c_int, bytes: u64, out: *mut *mut c_void) -> SdaStatus;
     pub fn sda_hbm_free(ptr: *mut c_void) -> SdaStatus;
+    pub fn sda_hbm_trim(device: c_int, keep_bytes: u64) -> SdaStatus;
+    pub fn sda_hbm_stats(device: c_int, live_bytes: *mut u64, pooled_bytes: *mut u64, retired_bytes: *mut u64)
+        -> SdaStatus;
 }

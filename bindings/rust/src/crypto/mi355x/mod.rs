@@ -46,6 +46,18 @@ impl Device {
         Ok(Arc::new(Device { h: Mutex::new(h) }))
     }
 
+    /// One handle over several GPUs (sda_engine_create_multi): the trait calls split their work over them
+    /// (a clerk's combine by columns, the recipient's ChaCha mask combine by seeds + one RCCL reduce) and
+    /// still return when the result is in host memory.
+    pub fn open_multi(ordinals: &[i32]) -> SdaClientResult<Arc<Device>> {
+        if unsafe { sda_abi_version() } != SDA_ENGINE_ABI_VERSION {
+            Err("libsda_engine ABI version mismatch")?
+        }
+        let mut h = std::ptr::null_mut();
+        check(unsafe { sda_engine_create_multi(ordinals.as_ptr(), ordinals.len() as i32, &mut h) })?;
+        Ok(Arc::new(Device { h: Mutex::new(h) }))
+    }
+
     fn call<F: FnOnce(*mut SdaEngine) -> SdaStatus>(&self, f: F) -> SdaClientResult<()> {
         let h = self.h.lock().unwrap();
         check(f(*h))

@@ -8,6 +8,8 @@
  * and client/src/crypto/masking/mod.rs:33-94.
  *
  * Conventions
+ *   - Host entry points stream their inputs through pinned double buffers in row tiles of
+ *     SDA_HOST_STAGE_MB (default 256) MiB, so a job larger than HBM runs (bit-identical to one pass).
  *   - Elements are i64 (client/src/crypto/mod.rs:33-36); arithmetic follows
  *     Rust: truncated `%`, wrapping `+` (release builds).
  *   - The caller owns every buffer.  Host entry points are synchronous (they
@@ -93,6 +95,18 @@ int sda_abi_version(void);
 sda_status sda_engine_create(int device_ordinal, sda_engine** out);
 void sda_engine_destroy(sda_engine* h);
 sda_status sda_engine_synchronize(sda_engine* h);
+/* One handle over n_devices devices ("1-8 GPUs are used internally").  The host entry
+ * points split their work over the devices and still return when the result is in host memory:
+ *   sda_share_combine / Full sda_mask_combine / Additive sda_secret_reconstruct: by columns (each device
+ *     walks every row in order over its slice: exact, signed inputs included, no exchange);
+ *   ChaCha sda_mask_combine: by seeds, one RCCL ncclReduce(SUM, int64) onto ordinals[0] + the device
+ *     finalize (RCCL is loaded on first use; moduli above 2^62, or repeated ordinals, run on ordinals[0]);
+ *   sda_share_generate / PackedShamir sda_secret_reconstruct: by batches (Additive generate: by columns).
+ * The `_dev` entry points run on ordinals[0].  Ordinals may repeat (several slices on one device: a
+ * rehearsal of the split on fewer GPUs).  n_devices = 1 gives a one-device handle whose ChaCha mask
+ * combine still reduces through a one-rank RCCL communicator. */
+sda_status sda_engine_create_multi(const int* ordinals, int n_devices, sda_engine** out);
+int sda_engine_device_count(const sda_engine* h);     /* devices the host entry points use; 0 for NULL */
 const char* sda_last_error_message(void);          /* thread-local; never NULL */
 const char* sda_status_string(int status);         /* reference error string for 1..6 */
 
@@ -339,12 +353,21 @@ sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64
  * Vec<i64> on the host, batched.rs:25-28).  `bytes` of device memory on `device`, one virtual range
  * mapped from physical chunks of SDA_HBM_CHUNK_MB (default 64) MiB, so its backing never depends on how
  * fragmented the driver's free VRAM is.  The range is rounded up to whole chunks.
- * sda_hbm_free waits for the device, then returns the buffer to a per-process pool: it stays mapped and a
- * later sda_hbm_alloc of up to its size (and at least half of it) gets it back; the memory is released when
- * the process ends.  NULL is a no-op; a pointer not returned by sda_hbm_alloc, or freed twice, is
- * INVALID_ARGUMENT. */
+ * sda_hbm_free does not wait: the buffer returns to a per-process pool, still mapped, and a later
+ * sda_hbm_alloc of up to its size (and at least half of it) gets it back (after a device-wide sync if it
+ * was freed since the allocator's last one).  The pool holds at most SDA_HBM_POOL_MB (default 32768) MiB
+ * per device: sda_hbm_alloc trims the oldest pooled buffers down to that bound first, and trims the whole
+ * pool and retries once when the device is out of memory.  Trimming syncs the device and releases the
+ * physical chunks; the virtual range stays reserved and is never mapped again (DESIGN.md §2 gives the
+ * cause).  NULL is a no-op; a pointer not returned by sda_hbm_alloc, or freed twice, is INVALID_ARGUMENT. */
 sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out);
 sda_status sda_hbm_free(void* ptr);
+/* Release pooled buffers of `device` (oldest first) until at most keep_bytes stay pooled.
+ * sda_engine_destroy trims its device's pool to 0. */
+sda_status sda_hbm_trim(int device, uint64_t keep_bytes);
+/* Bytes of `device` handed out, pooled (freed, mapped) and retired (virtual ranges kept reserved after a
+ * trim); any pointer may be NULL. */
+sda_status sda_hbm_stats(int device, uint64_t* live_bytes, uint64_t* pooled_bytes, uint64_t* retired_bytes);
 
 #ifdef __cplusplus
 }

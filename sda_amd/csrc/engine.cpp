@@ -7,15 +7,19 @@
 // the call fails.
 #include "../../include/sda_engine.h"
 
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels.h"
@@ -45,6 +49,18 @@ struct sda_engine {
     hipEvent_t order_ev = nullptr;
     bool order_ok = true;         // order_ev was recorded when the last call ended (else: host sync)
     unsigned long long* rej_host = nullptr;   // pinned: the ChaCha rejection count of a pipeline's mask
+    // streaming host path (host rows -> HBM in row tiles, host_path section): pinned staging and device
+    // tiles, double buffered, and a copy stream so a tile's upload overlaps the previous tile's combine
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t h2d_done[2] = {nullptr, nullptr}, tile_free[2] = {nullptr, nullptr};
+    void* hs_pin = nullptr;       // pinned host: 2 tiles
+    size_t hs_pin_bytes = 0;
+    void* hs_dev = nullptr;       // device: 2 tiles + the accumulator
+    size_t hs_dev_bytes = 0;
+    // a handle over G devices (sda_engine_create_multi): sub[0] is this handle, sub[1..G) are owned
+    // single-device handles; empty for a single-device handle
+    std::vector<sda_engine*> sub;
+    void** comms = nullptr;       // ncclComm_t[G], created on first use (RCCL, loaded at run time)
 };
 
 namespace {
@@ -172,18 +188,6 @@ sda_status check_packed(const sda_sharing_scheme* s) {
     return SDA_OK;
 }
 
-// upload n rows of `len` elements each into a dense [n][len] device buffer
-sda_status upload_rows(sda_engine* h, int64_t* dst, const int64_t* const* rows, uint64_t n, uint64_t len) {
-    uint64_t i = 0;
-    while (i < n) {
-        uint64_t j = i + 1;   // coalesce rows that are contiguous in host memory
-        while (j < n && rows[j] == rows[j - 1] + len) ++j;
-        if (len) HIP_TRY(hipMemcpyAsync(dst + i * len, rows[i], (j - i) * len * 8, hipMemcpyHostToDevice, h->stream));
-        i = j;
-    }
-    return SDA_OK;
-}
-
 struct DevArena {   // bump allocator over the engine's staging buffer
     char* base;
     size_t off = 0;
@@ -279,6 +283,19 @@ sda_status finish(sda_engine* h) {
     return ok();
 }
 
+// streaming, multi-device host path (defined at the end of this file)
+sda_status host_combine(sda_engine* h, int64_t m, const int64_t* const* rows, uint64_t n_rows, uint64_t dim,
+                        int64_t* out);
+sda_status host_chacha_combine(sda_engine* h, int64_t m, uint64_t D, const std::vector<uint32_t>& seeds, uint32_t w,
+                               uint64_t n, int64_t* out_host);
+void destroy_comms(sda_engine* h);
+sda_status host_additive_generate(sda_engine* h, int64_t m, uint64_t n, const int64_t* secrets, uint64_t D,
+                                  const int64_t* draws, int64_t* out);
+sda_status host_packed_generate(sda_engine* h, const sda_sharing_scheme* s, const int64_t* secrets, uint64_t D,
+                                const int64_t* draws, int64_t* out);
+sda_status host_packed_reconstruct(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,
+                                   const uint64_t* indices, const int64_t* const* rows, uint64_t n_rows, int64_t* out);
+
 }  // namespace
 
 extern "C" {
@@ -336,6 +353,11 @@ void sda_engine_destroy(sda_engine* h) {
     SDA_ENTRY;
     if (!h) return;
     if (t_call_h == h) t_call_h = nullptr;
+    if (h->comms) {                          // the handle's RCCL communicators (multi-device reduce)
+        destroy_comms(h);
+    }
+    for (size_t g = 1; g < h->sub.size(); ++g) sda_engine_destroy(h->sub[g]);
+    h->sub.clear();
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();            // _dev work may still be queued on callers' streams
     if (h->work) (void)hipFree(h->work);
@@ -348,8 +370,16 @@ void sda_engine_destroy(sda_engine* h) {
     sda::free_table(h->gen_tab);
     sda::free_table(h->rev_tab);
     if (h->rej_host) (void)hipHostFree(h->rej_host);
+    if (h->hs_pin) (void)hipHostFree(h->hs_pin);
+    if (h->hs_dev) (void)hipFree(h->hs_dev);
+    for (int b = 0; b < 2; ++b) {
+        if (h->h2d_done[b]) (void)hipEventDestroy(h->h2d_done[b]);
+        if (h->tile_free[b]) (void)hipEventDestroy(h->tile_free[b]);
+    }
+    if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
     if (h->order_ev) (void)hipEventDestroy(h->order_ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
+    (void)sda_hbm_trim(h->device, 0);        // the device's pooled sda_hbm_alloc buffers go back to the driver
     delete h;
 }
 
@@ -396,16 +426,9 @@ sda_status sda_share_generate(sda_engine* h, const sda_sharing_scheme* s, const 
                         (unsigned long long)(D * (n - 1)), (unsigned long long)n_draws);
         if (out_cap < n * D) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
         if (D == 0) return ok();
-        DevArena a;
-        if (sda_status st = stage(h, rup(D * 8) + rup(n_draws * 8) + rup(n * D * 8), &a)) return st;
-        int64_t* dsec = a.take<int64_t>(D);
-        int64_t* ddr = a.take<int64_t>(n_draws);
-        int64_t* dout = a.take<int64_t>(n * D);
-        HIP_TRY(hipMemcpyAsync(dsec, secrets, D * 8, hipMemcpyHostToDevice, h->stream));
-        if (n_draws) HIP_TRY(hipMemcpyAsync(ddr, draws, n_draws * 8, hipMemcpyHostToDevice, h->stream));
-        HIP_TRY(sda::launch_additive_generate(dsec, D, ddr, n, dout, s->modulus, h->stream));
-        HIP_TRY(hipMemcpyAsync(out, dout, n * D * 8, hipMemcpyDeviceToHost, h->stream));
-        return finish(h);
+        (void)pick(h, h->stream);
+        if (sda_status st = host_additive_generate(h, s->modulus, n, secrets, D, draws, out)) return st;
+        return ok();
     }
     if (s->kind != SDA_SHARING_PACKED_SHAMIR) return fail(SDA_ERR_INVALID_ARGUMENT, "unknown sharing scheme kind");
     if (sda_status st = check_packed(s)) return st;
@@ -416,20 +439,9 @@ sda_status sda_share_generate(sda_engine* h, const sda_sharing_scheme* s, const 
                     (unsigned long long)(B * t), (unsigned long long)n_draws);
     if (out_cap < n * B) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
     if (B == 0) return ok();
-    DevArena a;
-    if (sda_status st = stage(h, rup(D * 8) + rup(n_draws * 8) + rup(n * B * 8), &a)) return st;
-    int64_t* dsec = a.take<int64_t>(D);
-    int64_t* ddr = a.take<int64_t>(n_draws);
-    int64_t* dout = a.take<int64_t>(n * B);
-    HIP_TRY(hipMemcpyAsync(dsec, secrets, D * 8, hipMemcpyHostToDevice, h->stream));
-    if (n_draws) HIP_TRY(hipMemcpyAsync(ddr, draws, n_draws * 8, hipMemcpyHostToDevice, h->stream));
-    sda::PackedGenArgs ga{dsec, D, 1, ddr, dout};
-    if (sda_status st = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return st;
-    HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)k, (uint32_t)t, (uint32_t)n, (uint32_t)s->modulus,
-                                        (uint32_t)s->omega_secrets, (uint32_t)s->omega_shares, h->gen_tab,
-                                        h->gen_log, h->stream));
-    HIP_TRY(hipMemcpyAsync(out, dout, n * B * 8, hipMemcpyDeviceToHost, h->stream));
-    return finish(h);
+    (void)pick(h, h->stream);
+    if (sda_status st = host_packed_generate(h, s, secrets, D, draws, out)) return st;
+    return ok();
 }
 
 // ---------------- ShareCombiner::combine ----------------
@@ -458,14 +470,11 @@ static sda_status combine_rows(sda_engine* h, int64_t modulus, const int64_t* co
     if (dim == 0) return ok();
     for (uint64_t i = 0; i < n_rows; ++i)
         if (!rows[i]) return fail(SDA_ERR_INVALID_ARGUMENT, "row %llu is NULL", (unsigned long long)i);
-    DevArena a;
-    if (sda_status st = stage(h, rup(n_rows * dim * 8) + rup(dim * 8), &a)) return st;
-    int64_t* din = a.take<int64_t>(n_rows * dim);
-    int64_t* dout = a.take<int64_t>(dim);
-    if (sda_status st = upload_rows(h, din, rows, n_rows, dim)) return st;
-    HIP_TRY(sda::launch_combine_exact(din, n_rows, dim, dim, dout, m, h->stream));
-    HIP_TRY(hipMemcpyAsync(out, dout, dim * 8, hipMemcpyDeviceToHost, h->stream));
-    return finish(h);
+    (void)pick(h, h->stream);                  // host entry points run on the engine's own stream(s)
+    // row tiles through pinned double buffers, column slices over the handle's devices (host path section):
+    // jobs larger than HBM stream through, bit-identical to one pass
+    if (sda_status st = host_combine(h, m, rows, n_rows, dim, out)) return st;
+    return ok();
 }
 
 sda_status sda_share_combine(sda_engine* h, const sda_sharing_scheme* s, const int64_t* const* rows,
@@ -510,20 +519,10 @@ sda_status sda_secret_reconstruct(sda_engine* h, const sda_sharing_scheme* s, ui
                     (unsigned long long)n_rows, (unsigned long long)(s->privacy_threshold + k));
     if (n_rows > sda::kRevealMaxShares)
         return fail(SDA_ERR_UNSUPPORTED, "more than %u clerk shares per batch", sda::kRevealMaxShares);
-    DevArena a;
-    if (sda_status st = stage(h, rup(n_rows * B * 8) + rup(dimension * 8), &a)) return st;
-    int64_t* din = a.take<int64_t>(n_rows * B);
-    int64_t* dout = a.take<int64_t>(dimension);
-    for (uint64_t i = 0; i < n_rows; ++i)
-        HIP_TRY(hipMemcpyAsync(din + i * B, rows[i], B * 8, hipMemcpyHostToDevice, h->stream));
-    if (sda_status st = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return st;
-    sda::PackedRevealArgs ra{din, dimension, 1, dout};
-    HIP_TRY(sda::launch_packed_reveal(ra, indices, (uint32_t)n_rows, (uint32_t)k, (uint32_t)s->modulus,
-                                      (uint32_t)s->omega_secrets, (uint32_t)s->omega_shares, SDA_REVEAL_EXACT,
-                                      h->rev_tab, h->gen_log, h->stream));
-    HIP_TRY(hipMemcpyAsync(out, dout, dimension * 8, hipMemcpyDeviceToHost, h->stream));
+    (void)pick(h, h->stream);
+    if (sda_status st = host_packed_reconstruct(h, s, dimension, indices, rows, n_rows, out)) return st;
     *out_len = dimension;
-    return finish(h);
+    return ok();
 }
 
 // ---------------- masking ----------------
@@ -613,15 +612,9 @@ sda_status sda_mask_combine(sda_engine* h, const sda_masking_scheme* s, const in
         for (uint64_t j = 0; j < lens[i] && j < w; ++j) seeds[i * w + j] = (uint32_t)rows[i][j];   // chacha.rs:62-64
     *out_len = D;
     if (D == 0) return ok();
-    DevArena a;
-    if (sda_status st = stage(h, rup(seeds.size() * 4 + 4) + rup(D * 8), &a)) return st;
-    uint32_t* dseeds = a.take<uint32_t>(seeds.size() + 1);
-    int64_t* dout = a.take<int64_t>(D);
-    if (!seeds.empty())
-        HIP_TRY(hipMemcpyAsync(dseeds, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, h->stream));
-    if (sda_status st = chacha_combine(h, s->modulus, D, dseeds, (uint32_t)w, n_rows, dout, h->stream)) return st;
-    HIP_TRY(hipMemcpyAsync(out, dout, D * 8, hipMemcpyDeviceToHost, h->stream));
-    return finish(h);
+    // seeds split over the handle's devices, one RCCL reduce (host path section); one device: all seeds
+    if (sda_status st = host_chacha_combine(h, s->modulus, D, seeds, (uint32_t)w, n_rows, out)) return st;
+    return ok();
 }
 
 sda_status sda_secret_unmask(sda_engine* h, const sda_masking_scheme* s, const int64_t* mask, uint64_t mask_len,
@@ -866,20 +859,42 @@ sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64
 // case measured, whatever the chunk size (2 MiB - 1 GiB) and whether the chunks were mapped in order or
 // shuffled (profiles/r04r).  sda_hbm_alloc / sda_hbm_free give the resident hot-path buffers that backing.
 //
-// A freed buffer stays mapped, in a per-process pool that later allocations reuse (best fit, at most twice
-// the size asked for).  Unmapping and releasing a buffer, then letting the runtime hand its virtual range to
-// other allocations, corrupted data in the GPU suite (profiles/r04y: reads of a torch temporary returned a
-// different count each time), so no range is ever unmapped while the process runs.
+// Life cycle ("HBM backing"):
+//   - sda_hbm_free never waits: the buffer goes to a per-process pool, still mapped, stamped with the
+//     device's sync epoch.  Work queued on any stream may still use it.  (SDA_HBM_POOL_MB=0 disables the
+//     pool: free then syncs the device and releases the buffer at once.)
+//   - sda_hbm_alloc hands out the smallest pooled buffer that fits (at most twice the size asked for); one
+//     freed since the last device-wide sync costs a hipDeviceSynchronize first.
+//   - The pool is bounded: SDA_HBM_POOL_MB (default 32768) per device.  An allocation first trims the
+//     oldest pooled buffers down to the bound; an allocation that hits OUT_OF_MEMORY trims the whole pool
+//     and retries once; sda_hbm_trim and sda_engine_destroy trim explicitly.
+//   - Trimming syncs the device, unmaps the chunks and releases them (the HBM returns to the driver), but
+//     the VIRTUAL range stays reserved, retired, for the life of the process: it is never mapped again.
+//     Cause (profiles/r05b/hbm_repro_suite_sequence.txt): when a freed range was also returned with
+//     hipMemAddressFree, the next hipMemAddressReserve of the same size handed the same range out again, and
+//     the GPU's view of the new mapping was inconsistent -- in the suite's own sequence (a buffer touched by
+//     torch kernels, freed, the same size allocated at once) `fill_(-1)` followed by `max()` read 0s (twice out
+//     of twice), as r04y's share-gen buffer read back a different zero count on every read.  With the range
+//     retired the same sequence passes (twice out of twice), as does the whole suite.  Retired ranges cost
+//     only address space (2^47 bytes of it per process).  SDA_HBM_VA_FREE=1 restores the address free for
+//     that A/B (scripts/hbm_repro.sh).
 namespace {
 
 struct HbmBuffer {
     int device = 0;
     size_t bytes = 0;                                   // reserved (a whole number of chunks)
+    size_t chunk = 0;
     std::vector<hipMemGenericAllocationHandle_t> chunks;
+    uint64_t freed_epoch = 0;                           // pool only: the device's sync epoch at free time
+    uint64_t freed_seq = 0;                             // pool only: free order (oldest is trimmed first)
 };
 std::mutex g_hbm_mu;
 std::map<uintptr_t, HbmBuffer> g_hbm;                   // handed out
 std::map<uintptr_t, HbmBuffer> g_hbm_pool;              // freed, still mapped
+constexpr int kHbmMaxDev = 64;
+uint64_t g_hbm_epoch[kHbmMaxDev];                       // device-wide syncs done by the allocator
+uint64_t g_hbm_retired[kHbmMaxDev];                     // bytes of virtual ranges retired (never remapped)
+uint64_t g_hbm_seq = 0;
 
 size_t hbm_chunk_bytes() {
     const char* e = getenv("SDA_HBM_CHUNK_MB");
@@ -887,11 +902,92 @@ size_t hbm_chunk_bytes() {
     return (size_t)(mb > 0 ? mb : 64) << 20;
 }
 
-// unmap and release what a partly built buffer holds (the failure path of sda_hbm_alloc only)
-void hbm_release(void* ptr, HbmBuffer& b, size_t mapped_chunks, size_t chunk) {
-    for (size_t i = 0; i < mapped_chunks; ++i) (void)hipMemUnmap(static_cast<char*>(ptr) + i * chunk, chunk);
+uint64_t hbm_pool_cap() {
+    const char* e = getenv("SDA_HBM_POOL_MB");
+    const long long mb = e ? atoll(e) : 32768;
+    return (uint64_t)(mb > 0 ? mb : 0) << 20;
+}
+
+bool hbm_va_free() {
+    const char* e = getenv("SDA_HBM_VA_FREE");
+    return e && atoi(e) == 1;
+}
+
+// unmap and release the first `mapped_chunks` chunks' mappings and every chunk handle; the virtual range is
+// retired (kept reserved) unless SDA_HBM_VA_FREE=1.  The caller has made sure no queued work uses it.
+void hbm_release(void* ptr, HbmBuffer& b, size_t mapped_chunks) {
+    for (size_t i = 0; i < mapped_chunks; ++i) (void)hipMemUnmap(static_cast<char*>(ptr) + i * b.chunk, b.chunk);
     for (auto& c : b.chunks) (void)hipMemRelease(c);
-    if (ptr) (void)hipMemAddressFree(ptr, b.bytes);
+    b.chunks.clear();
+    if (!ptr) return;
+    if (hbm_va_free())
+        (void)hipMemAddressFree(ptr, b.bytes);
+    else if (b.device >= 0 && b.device < kHbmMaxDev)
+        g_hbm_retired[b.device] += b.bytes;
+}
+
+uint64_t hbm_pooled_bytes(int device) {   // g_hbm_mu held
+    uint64_t s = 0;
+    for (auto& kv : g_hbm_pool)
+        if (kv.second.device == device) s += kv.second.bytes;
+    return s;
+}
+
+// Trim the device's pool (oldest first) until at most `keep` bytes stay pooled.  g_hbm_mu held; the
+// device is current.  One device-wide sync covers every buffer trimmed.
+hipError_t hbm_trim_locked(int device, uint64_t keep) {
+    uint64_t pooled = hbm_pooled_bytes(device);
+    if (pooled <= keep) return hipSuccess;
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return e;
+    ++g_hbm_epoch[device];
+    while (pooled > keep) {
+        auto old = g_hbm_pool.end();
+        for (auto it = g_hbm_pool.begin(); it != g_hbm_pool.end(); ++it)
+            if (it->second.device == device && (old == g_hbm_pool.end() || it->second.freed_seq < old->second.freed_seq))
+                old = it;
+        if (old == g_hbm_pool.end()) break;
+        pooled -= old->second.bytes;
+        hbm_release(reinterpret_cast<void*>(old->first), old->second, old->second.chunks.size());
+        g_hbm_pool.erase(old);
+    }
+    return hipSuccess;
+}
+
+// Reserve + map a new buffer of n chunks.
+hipError_t hbm_create(int device, size_t n, size_t chunk, const hipMemAllocationProp& prop, void** out, HbmBuffer* b) {
+    b->device = device;
+    b->bytes = n * chunk;
+    b->chunk = chunk;
+    void* ptr = nullptr;
+    hipError_t e = hipMemAddressReserve(&ptr, b->bytes, chunk, nullptr, 0);
+    if (e != hipSuccess) return e;
+    b->chunks.reserve(n);
+    size_t mapped = 0;
+    for (size_t i = 0; i < n && e == hipSuccess; ++i) {
+        hipMemGenericAllocationHandle_t c;
+        e = hipMemCreate(&c, chunk, &prop, 0);
+        if (e != hipSuccess) break;
+        b->chunks.push_back(c);
+        e = hipMemMap(static_cast<char*>(ptr) + i * chunk, chunk, 0, c, 0);
+        if (e == hipSuccess) ++mapped;
+    }
+    if (e == hipSuccess) {
+        hipMemAccessDesc acc = {};
+        acc.location = prop.location;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        e = hipMemSetAccess(ptr, b->bytes, &acc, 1);
+    }
+    if (e != hipSuccess) {
+        // never mapped for a kernel (hipMemSetAccess is the last step), so the range may go back as well
+        for (size_t i = 0; i < mapped; ++i) (void)hipMemUnmap(static_cast<char*>(ptr) + i * chunk, chunk);
+        for (auto& c : b->chunks) (void)hipMemRelease(c);
+        b->chunks.clear();
+        (void)hipMemAddressFree(ptr, b->bytes);
+        return e;
+    }
+    *out = ptr;
+    return hipSuccess;
 }
 
 }  // namespace
@@ -910,6 +1006,7 @@ sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out) {
     if (!out) return fail(SDA_ERR_INVALID_ARGUMENT, "out is NULL");
     *out = nullptr;
     if (bytes == 0) return fail(SDA_ERR_INVALID_ARGUMENT, "bytes must be > 0");
+    if (device < 0 || device >= kHbmMaxDev) return fail(SDA_ERR_INVALID_ARGUMENT, "device %d out of range", device);
     DeviceGuard dg;
     HIP_TRY(hipSetDevice(device));
     hipMemAllocationProp prop = {};
@@ -921,8 +1018,9 @@ sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out) {
     if (gran == 0) gran = 4096;
     const size_t chunk = (hbm_chunk_bytes() + gran - 1) / gran * gran;
     const size_t n = (size_t)((bytes + chunk - 1) / chunk);
+    std::lock_guard<std::mutex> lk(g_hbm_mu);
+    HIP_TRY(hbm_trim_locked(device, hbm_pool_cap()));
     {   // a pooled buffer of this device that fits, the smallest one (at most twice the size)
-        std::lock_guard<std::mutex> lk(g_hbm_mu);
         auto best = g_hbm_pool.end();
         for (auto it = g_hbm_pool.begin(); it != g_hbm_pool.end(); ++it) {
             const HbmBuffer& c = it->second;
@@ -931,6 +1029,10 @@ sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out) {
                 best = it;
         }
         if (best != g_hbm_pool.end()) {
+            if (best->second.freed_epoch == g_hbm_epoch[device]) {   // freed since the last sync: may be in use
+                HIP_TRY(hipDeviceSynchronize());
+                ++g_hbm_epoch[device];
+            }
             *out = reinterpret_cast<void*>(best->first);
             g_hbm[best->first] = std::move(best->second);
             g_hbm_pool.erase(best);
@@ -938,38 +1040,21 @@ sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out) {
         }
     }
     HbmBuffer b;
-    b.device = device;
-    b.bytes = n * chunk;
     void* ptr = nullptr;
-    HIP_TRY(hipMemAddressReserve(&ptr, b.bytes, chunk, nullptr, 0));
-    b.chunks.reserve(n);
-    size_t mapped = 0;
-    hipError_t e = hipSuccess;
-    for (size_t i = 0; i < n && e == hipSuccess; ++i) {
-        hipMemGenericAllocationHandle_t c;
-        e = hipMemCreate(&c, chunk, &prop, 0);
-        if (e != hipSuccess) break;
-        b.chunks.push_back(c);
-        e = hipMemMap(static_cast<char*>(ptr) + i * chunk, chunk, 0, c, 0);
-        if (e == hipSuccess) ++mapped;
-    }
-    if (e == hipSuccess) {
-        hipMemAccessDesc acc = {};
-        acc.location = prop.location;
-        acc.flags = hipMemAccessFlagsProtReadWrite;
-        e = hipMemSetAccess(ptr, b.bytes, &acc, 1);
+    hipError_t e = hbm_create(device, n, chunk, prop, &ptr, &b);
+    if (e == hipErrorOutOfMemory && hbm_pooled_bytes(device) > 0) {   // give the pool back, then retry once
+        (void)hipGetLastError();
+        HIP_TRY(hbm_trim_locked(device, 0));
+        b = HbmBuffer();
+        e = hbm_create(device, n, chunk, prop, &ptr, &b);
     }
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        hbm_release(ptr, b, mapped, chunk);
         return fail(e == hipErrorOutOfMemory ? SDA_ERR_OUT_OF_MEMORY : SDA_ERR_DEVICE,
                     "sda_hbm_alloc(%llu bytes in %zu MiB chunks): %s", (unsigned long long)bytes, chunk >> 20,
                     hipGetErrorString(e));
     }
-    {
-        std::lock_guard<std::mutex> lk(g_hbm_mu);
-        g_hbm[reinterpret_cast<uintptr_t>(ptr)] = std::move(b);
-    }
+    g_hbm[reinterpret_cast<uintptr_t>(ptr)] = std::move(b);
     *out = ptr;
     return ok();
 }
@@ -977,22 +1062,45 @@ sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out) {
 sda_status sda_hbm_free(void* ptr) {
     SDA_ENTRY;
     if (!ptr) return ok();
-    int device = 0;
-    {
-        std::lock_guard<std::mutex> lk(g_hbm_mu);
-        auto it = g_hbm.find(reinterpret_cast<uintptr_t>(ptr));
-        if (it == g_hbm.end()) return fail(SDA_ERR_INVALID_ARGUMENT, "%p was not returned by sda_hbm_alloc", ptr);
-        device = it->second.device;
-    }
-    // work queued on any stream may still use the buffer: it returns to the pool once the device is idle
-    DeviceGuard dg;
-    HIP_TRY(hipSetDevice(device));
-    HIP_TRY(hipDeviceSynchronize());
     std::lock_guard<std::mutex> lk(g_hbm_mu);
     auto it = g_hbm.find(reinterpret_cast<uintptr_t>(ptr));
-    if (it == g_hbm.end()) return fail(SDA_ERR_INVALID_ARGUMENT, "%p was freed twice", ptr);
+    if (it == g_hbm.end()) return fail(SDA_ERR_INVALID_ARGUMENT, "%p was not returned by sda_hbm_alloc (or freed twice)", ptr);
+    if (hbm_pool_cap() == 0) {   // no pool (SDA_HBM_POOL_MB=0): release at once, after the device is idle
+        DeviceGuard dg;
+        HIP_TRY(hipSetDevice(it->second.device));
+        HIP_TRY(hipDeviceSynchronize());
+        ++g_hbm_epoch[it->second.device];
+        hbm_release(ptr, it->second, it->second.chunks.size());
+        g_hbm.erase(it);
+        return ok();
+    }
+    it->second.freed_epoch = g_hbm_epoch[it->second.device];
+    it->second.freed_seq = ++g_hbm_seq;
     g_hbm_pool[it->first] = std::move(it->second);
     g_hbm.erase(it);
+    return ok();
+}
+
+sda_status sda_hbm_trim(int device, uint64_t keep_bytes) {
+    SDA_ENTRY;
+    if (device < 0 || device >= kHbmMaxDev) return fail(SDA_ERR_INVALID_ARGUMENT, "device %d out of range", device);
+    DeviceGuard dg;
+    HIP_TRY(hipSetDevice(device));
+    std::lock_guard<std::mutex> lk(g_hbm_mu);
+    HIP_TRY(hbm_trim_locked(device, keep_bytes));
+    return ok();
+}
+
+sda_status sda_hbm_stats(int device, uint64_t* live_bytes, uint64_t* pooled_bytes, uint64_t* retired_bytes) {
+    SDA_ENTRY;
+    if (device < 0 || device >= kHbmMaxDev) return fail(SDA_ERR_INVALID_ARGUMENT, "device %d out of range", device);
+    std::lock_guard<std::mutex> lk(g_hbm_mu);
+    uint64_t live = 0;
+    for (auto& kv : g_hbm)
+        if (kv.second.device == device) live += kv.second.bytes;
+    if (live_bytes) *live_bytes = live;
+    if (pooled_bytes) *pooled_bytes = hbm_pooled_bytes(device);
+    if (retired_bytes) *retired_bytes = g_hbm_retired[device];
     return ok();
 }
 
@@ -1414,9 +1522,23 @@ sda_status recipient_pipeline(sda_engine* h, const sda_masking_scheme* ms, const
         }
         if (sda_status e = ensure(&h->gen_log, &h->gen_log_bytes, sda::packed_gen_log_bytes())) return e;
         sda::PackedRevealArgs ra{src, dimension, 1, dmasked};
+        // The output is positive(unmask(reveal)).  When the masking modulus (or no mask) and output_modulus are
+        // both the sharing prime, that is the canonical residue of (reveal - mask) mod p, which depends only on
+        // the reveal's residue: tss' signed representatives (EXACT, 2.1x the canonical reveal's time) cannot
+        // change a byte of it, so the canonical reveal runs.  Duplicate clerk points (no Lagrange form) fall
+        // back to EXACT.  SDA_RECIPIENT_EXACT=1 keeps EXACT (A/B and test knob).
+        const int64_t p = ss->modulus;
+        const char* keep = getenv("SDA_RECIPIENT_EXACT");
+        const bool residue_only = output_modulus == p && (ms->kind == SDA_MASKING_NONE || q == p) &&
+                                  !(keep && atoi(keep) == 1);
+        const int32_t run_mode = (mode == SDA_REVEAL_EXACT && residue_only) ? SDA_REVEAL_CANONICAL : mode;
         hipError_t e = sda::launch_packed_reveal(ra, indices, (uint32_t)n_idx, (uint32_t)ss->secret_count,
-                                                 (uint32_t)ss->modulus, (uint32_t)ss->omega_secrets,
-                                                 (uint32_t)ss->omega_shares, mode, h->rev_tab, h->gen_log, st);
+                                                 (uint32_t)p, (uint32_t)ss->omega_secrets,
+                                                 (uint32_t)ss->omega_shares, run_mode, h->rev_tab, h->gen_log, st);
+        if (e == hipErrorInvalidValue && run_mode != mode)
+            e = sda::launch_packed_reveal(ra, indices, (uint32_t)n_idx, (uint32_t)ss->secret_count, (uint32_t)p,
+                                          (uint32_t)ss->omega_secrets, (uint32_t)ss->omega_shares, mode, h->rev_tab,
+                                          h->gen_log, st);
         if (e == hipErrorInvalidValue && mode == SDA_REVEAL_CANONICAL)
             return fail(SDA_ERR_UNSUPPORTED, "canonical reveal needs distinct clerk indices");
         HIP_TRY(e);
@@ -1618,5 +1740,432 @@ sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms
     }
     return ok();
 }
+
+}  // extern "C"
+
+// ---------------- streaming, multi-device host path ----------------
+// The host entry points take the reference's host buffers (a Vec<Vec<i64>> of rows, clerk.rs:79-86) and
+// return when the result is in host memory.  A clerk job may be larger than HBM, so rows never sit in one
+// device buffer: each device streams them in row tiles through two pinned host buffers and two device tiles
+// (host_stage_bytes() each).  Tile i is packed on the host (host threads copying the rows' column slice into
+// pinned memory) while tile i - 1 uploads on the copy stream and tile i - 2's combine runs on the compute
+// stream; the combine continues the recurrence across tiles (launch_combine_exact, accumulate), so the
+// result is bit-identical to one pass over all rows.
+//
+// A handle over G devices (sda_engine_create_multi) splits the host calls:
+//   - combine (ShareCombiner, Full MaskCombiner, Additive reconstruct): by COLUMNS.  Device g walks every
+//     row, in order, over its column slice and writes that slice of the result: exact for signed inputs in
+//     one pass with no exchange.  A participation split would have to stream a signed
+//     job's rows over PCIe twice (DESIGN.md §5's two-pass split), and the rows come from the host anyway.
+//   - ChaCha MaskCombiner: by SEEDS (the expansion is compute-bound, the rows are a few words).  Each device
+//     sums its seeds' canonical draws; one RCCL ncclReduce(SUM, int64) over xGMI onto device 0 and the
+//     device finalize give the reference's result (every draw is >= 0; headroom G (m - 1) <= 2^63 - 1 is
+//     checked).  Moduli above 2^62 (the reference's own sum wraps there) and handles whose ordinals repeat
+//     run on device 0 alone.
+//   - packed share generate / reconstruct: by BATCHES; additive share generate: by columns.
+namespace {
+
+long long env_ll(const char* name, long long dflt) {
+    const char* e = getenv(name);
+    return e && *e ? atoll(e) : dflt;
+}
+
+// host threads for packing rows into pinned memory (SDA_HOST_THREADS; default: the CPUs, at most 16)
+int host_threads() {
+    const long long t = env_ll("SDA_HOST_THREADS", 0);
+    if (t > 0) return (int)std::min<long long>(t, 256);
+    const unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hc ? hc : 1u, 16u));
+}
+
+// bytes of one staging tile (SDA_HOST_STAGE_MB, default 256 MiB; at least 1 MiB)
+uint64_t host_stage_bytes() {
+    const long long mb = env_ll("SDA_HOST_STAGE_MB", 256);
+    return (uint64_t)std::max<long long>(mb, 1) << 20;
+}
+
+// copy the column slice [lo, lo + w) of rows [r0, r0 + R) into dst ([R][w], dense) on `threads` threads
+void pack_rows(int64_t* dst, const int64_t* const* rows, uint64_t r0, uint64_t R, uint64_t lo, uint64_t w,
+               int threads) {
+    const uint64_t total = R * w;
+    auto work = [=](uint64_t e0, uint64_t e1) {
+        while (e0 < e1) {
+            const uint64_t r = e0 / w, c = e0 % w;
+            const uint64_t n = std::min(e1 - e0, w - c);
+            memcpy(dst + e0, rows[r0 + r] + lo + c, n * 8);
+            e0 += n;
+        }
+    };
+    const uint64_t min_per_thread = 512 * 1024;             // elements (4 MiB): smaller pieces are not worth a thread
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, total / min_per_thread));
+    if (T <= 1) {
+        work(0, total);
+        return;
+    }
+    const uint64_t per = (total + T - 1) / T;
+    std::vector<std::thread> ts;
+    ts.reserve(T - 1);
+    for (int t = 1; t < T; ++t) {
+        const uint64_t e0 = std::min(total, (uint64_t)t * per), e1 = std::min(total, e0 + per);
+        if (e0 < e1) ts.emplace_back(work, e0, e1);
+    }
+    work(0, std::min(per, total));
+    for (auto& t : ts) t.join();
+}
+
+sda_status host_stream_ensure(sda_engine* h, size_t tile_bytes, size_t acc_bytes) {
+    if (!h->copy_stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+        for (int b = 0; b < 2; ++b) {
+            HIP_TRY(hipEventCreateWithFlags(&h->h2d_done[b], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&h->tile_free[b], hipEventDisableTiming));
+        }
+    }
+    if (h->hs_pin_bytes < 2 * rup(tile_bytes)) {
+        if (h->hs_pin) (void)hipHostFree(h->hs_pin);
+        h->hs_pin = nullptr;
+        h->hs_pin_bytes = 0;
+        HIP_TRY(hipHostMalloc(&h->hs_pin, 2 * rup(tile_bytes), hipHostMallocDefault));
+        h->hs_pin_bytes = 2 * rup(tile_bytes);
+    }
+    const size_t dev_need = 2 * rup(tile_bytes) + rup(acc_bytes);
+    if (h->hs_dev_bytes < dev_need) {
+        if (h->hs_dev) (void)hipFree(h->hs_dev);
+        h->hs_dev = nullptr;
+        h->hs_dev_bytes = 0;
+        HIP_TRY(hipMalloc(&h->hs_dev, dev_need));
+        h->hs_dev_bytes = dev_need;
+    }
+    return SDA_OK;
+}
+
+// combiner.rs:22-25 (|m| > 0) over the column slice [lo, lo + w) of n_rows host rows on h's device, streamed
+// in row tiles (section comment); the w results land in out_host.  A row slice wider than a tile is taken in
+// column chunks, each a full pass over the rows.
+sda_status stream_combine_slice(sda_engine* h, int64_t m, const int64_t* const* rows, uint64_t n_rows, uint64_t lo,
+                                uint64_t w, int64_t* out_host, int threads) {
+    HIP_TRY(hipSetDevice(h->device));
+    const uint64_t stage = host_stage_bytes();
+    const uint64_t wc_max = std::max<uint64_t>(2, stage / 8 / 2 * 2);
+    for (uint64_t c0 = 0; c0 < w; c0 += wc_max) {
+        const uint64_t wc = std::min(wc_max, w - c0);
+        const uint64_t R = std::max<uint64_t>(1, stage / (wc * 8));
+        const size_t tile = (size_t)(std::min(R, std::max<uint64_t>(n_rows, 1)) * wc * 8);
+        if (sda_status e = host_stream_ensure(h, tile, wc * 8)) return e;
+        int64_t* dt[2] = {static_cast<int64_t*>(h->hs_dev), static_cast<int64_t*>(h->hs_dev) + rup(tile) / 8};
+        int64_t* acc = static_cast<int64_t*>(h->hs_dev) + 2 * rup(tile) / 8;
+        int64_t* hp[2] = {static_cast<int64_t*>(h->hs_pin), static_cast<int64_t*>(h->hs_pin) + rup(tile) / 8};
+        uint64_t i = 0;
+        for (uint64_t r0 = 0; r0 < n_rows; r0 += R, ++i) {
+            const uint64_t Ri = std::min(R, n_rows - r0);
+            const int b = (int)(i & 1);
+            if (i >= 2) HIP_TRY(hipEventSynchronize(h->h2d_done[b]));        // tile i - 2 has left hp[b]
+            pack_rows(hp[b], rows, r0, Ri, lo + c0, wc, threads);
+            if (i >= 2) HIP_TRY(hipStreamWaitEvent(h->copy_stream, h->tile_free[b], 0));   // ... and dt[b]
+            HIP_TRY(hipMemcpyAsync(dt[b], hp[b], Ri * wc * 8, hipMemcpyHostToDevice, h->copy_stream));
+            HIP_TRY(hipEventRecord(h->h2d_done[b], h->copy_stream));
+            HIP_TRY(hipStreamWaitEvent(h->stream, h->h2d_done[b], 0));
+            HIP_TRY(sda::launch_combine_exact(dt[b], Ri, wc, wc, acc, m, h->stream, i > 0));
+            HIP_TRY(hipEventRecord(h->tile_free[b], h->stream));
+        }
+        HIP_TRY(hipMemcpyAsync(out_host + c0, acc, wc * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    return SDA_OK;
+}
+
+size_t n_devices(const sda_engine* h) { return h->sub.empty() ? 1 : h->sub.size(); }
+
+// run fn(g) for every device of the handle, one host thread per device (fn(0) on the caller's thread); the first
+// failing device's status and message are returned
+template <typename F>
+sda_status for_devices(sda_engine* h, F fn) {
+    const size_t G = n_devices(h);
+    if (G == 1) return fn(0);
+    std::vector<sda_status> st(G, SDA_OK);
+    std::vector<std::string> msg(G);
+    std::vector<std::thread> ts;
+    for (size_t g = 1; g < G; ++g)
+        ts.emplace_back([&, g] {
+            st[g] = fn(g);
+            if (st[g]) msg[g] = g_last_error;
+        });
+    st[0] = fn(0);
+    if (st[0]) msg[0] = g_last_error;
+    for (auto& t : ts) t.join();
+    for (size_t g = 0; g < G; ++g)
+        if (st[g]) return fail(st[g], "device %d: %s", h->sub[g]->device, msg[g].c_str());
+    return SDA_OK;
+}
+
+// even-aligned column split (sda_amd/distributed.py column_slice): [lo, lo + w) of dim for part g of G
+void column_slice(uint64_t dim, size_t g, size_t G, uint64_t* lo, uint64_t* w) {
+    const uint64_t pairs = (dim + 1) / 2, base = pairs / G, extra = pairs % G;
+    const uint64_t start = g * base + std::min<uint64_t>(g, extra), count = base + (g < extra ? 1 : 0);
+    *lo = std::min(dim, 2 * start);
+    *w = std::min(dim, 2 * (start + count)) - *lo;
+}
+
+// contiguous near-equal split of n items (shard_range)
+void shard(uint64_t n, size_t g, size_t G, uint64_t* start, uint64_t* count) {
+    const uint64_t base = n / G, extra = n % G;
+    *start = g * base + std::min<uint64_t>(g, extra);
+    *count = base + (g < extra ? 1 : 0);
+}
+
+sda_engine* dev_of(sda_engine* h, size_t g) { return h->sub.empty() ? h : h->sub[g]; }
+
+// combiner.rs:16-28 over host rows (validated by combine_rows): one device streams all columns, G devices
+// a column slice each
+sda_status host_combine(sda_engine* h, int64_t m, const int64_t* const* rows, uint64_t n_rows, uint64_t dim,
+                        int64_t* out) {
+    const size_t G = n_devices(h);
+    const int T = std::max(1, host_threads() / (int)G);
+    return for_devices(h, [&](size_t g) -> sda_status {
+        uint64_t lo, w;
+        column_slice(dim, g, G, &lo, &w);
+        if (w == 0) return SDA_OK;
+        return stream_combine_slice(dev_of(h, g), m, rows, n_rows, lo, w, out + lo, T);
+    });
+}
+
+// ---- RCCL, loaded when a multi-device handle first reduces (single-device users never load it) ----
+struct Rccl {
+    bool ok = false;
+    std::string err;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t,
+                           hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!lib) {
+            r.err = dlerror() ? dlerror() : "dlopen(librccl.so.1) failed";
+            return;
+        }
+        r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(lib, "ncclCommInitAll"));
+        r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(lib, "ncclCommDestroy"));
+        r.reduce = reinterpret_cast<decltype(r.reduce)>(dlsym(lib, "ncclReduce"));
+        r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(lib, "ncclGroupStart"));
+        r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(lib, "ncclGroupEnd"));
+        r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(lib, "ncclGetErrorString"));
+        r.ok = r.comm_init_all && r.comm_destroy && r.reduce && r.group_start && r.group_end && r.error_string;
+        if (!r.ok) r.err = "librccl.so.1 lacks an entry point";
+    });
+    return r;
+}
+
+#define NCCL_TRY(expr)                                                                                  \
+    do {                                                                                                \
+        ncclResult_t _r = (expr);                                                                       \
+        if (_r != ncclSuccess)                                                                          \
+            return fail(SDA_ERR_DEVICE, "%s failed: %s (%s:%d)", #expr, rccl().error_string(_r), __FILE__, \
+                        __LINE__);                                                                      \
+    } while (0)
+
+bool distinct_devices(const sda_engine* h) {
+    for (size_t a = 0; a < h->sub.size(); ++a)
+        for (size_t b = a + 1; b < h->sub.size(); ++b)
+            if (h->sub[a]->device == h->sub[b]->device) return false;
+    return true;
+}
+
+sda_status ensure_comms(sda_engine* h) {
+    if (h->comms) return SDA_OK;
+    Rccl& r = rccl();
+    if (!r.ok) return fail(SDA_ERR_DEVICE, "RCCL unavailable: %s", r.err.c_str());
+    const size_t G = n_devices(h);
+    std::vector<int> devs(G);
+    for (size_t g = 0; g < G; ++g) devs[g] = dev_of(h, g)->device;
+    std::vector<ncclComm_t> comms(G, nullptr);
+    NCCL_TRY(r.comm_init_all(comms.data(), (int)G, devs.data()));
+    h->comms = new void*[G];
+    for (size_t g = 0; g < G; ++g) h->comms[g] = comms[g];
+    return SDA_OK;
+}
+
+void destroy_comms(sda_engine* h) {
+    if (!h->comms) return;
+    for (size_t g = 0; g < n_devices(h); ++g)
+        if (h->comms[g]) (void)rccl().comm_destroy(static_cast<ncclComm_t>(h->comms[g]));
+    delete[] h->comms;
+    h->comms = nullptr;
+}
+
+// chacha.rs:57-76 over host seed words [n][w] (combined into out_host, D values): seeds split over the devices,
+// one RCCL reduce onto device 0 (section comment)
+sda_status host_chacha_combine(sda_engine* h, int64_t m, uint64_t D, const std::vector<uint32_t>& seeds, uint32_t w,
+                               uint64_t n, int64_t* out_host) {
+    // (a one-device handle from sda_engine_create_multi takes the split path too: a one-rank reduce)
+    const size_t G = n_devices(h);
+    const bool split = !h->sub.empty() && distinct_devices(h) && n >= G && !sda::chacha_needs_stream_path(m) &&
+                       (unsigned __int128)G * (uint64_t)(m - 1) <= (unsigned __int128)INT64_MAX;
+    const size_t parts = split ? G : 1;
+    std::vector<int64_t*> partial(parts, nullptr);
+    sda_status st = for_devices(h, [&](size_t g) -> sda_status {
+        if (g >= parts) return SDA_OK;
+        sda_engine* d = dev_of(h, g);
+        HIP_TRY(hipSetDevice(d->device));
+        uint64_t s0 = 0, cnt = n;
+        if (split) shard(n, g, G, &s0, &cnt);
+        DevArena a;
+        if (sda_status e = stage(d, rup(cnt * w * 4 + 4) + 2 * rup(D * 8), &a)) return e;
+        uint32_t* dseeds = a.take<uint32_t>(cnt * w + 1);
+        partial[g] = a.take<int64_t>(D);
+        if (cnt) HIP_TRY(hipMemcpyAsync(dseeds, seeds.data() + s0 * w, cnt * w * 4, hipMemcpyHostToDevice, d->stream));
+        return chacha_combine(d, m, D, dseeds, w, cnt, partial[g], d->stream);
+    });
+    if (st) return st;
+    int64_t* res = partial[0];
+    if (split) {
+        if (sda_status e = ensure_comms(h)) return e;
+        Rccl& r = rccl();
+        NCCL_TRY(r.group_start());
+        for (size_t g = 0; g < G; ++g) {
+            sda_engine* d = dev_of(h, g);
+            ncclResult_t rr = r.reduce(partial[g], partial[g], D, ncclInt64, ncclSum, 0,
+                                       static_cast<ncclComm_t>(h->comms[g]), d->stream);
+            if (rr != ncclSuccess) {
+                (void)r.group_end();
+                return fail(SDA_ERR_DEVICE, "ncclReduce: %s", r.error_string(rr));
+            }
+        }
+        NCCL_TRY(r.group_end());
+        HIP_TRY(hipSetDevice(h->device));
+        res = partial[0] + rup(D * 8) / 8;                     // the arena's second D-slot on device 0
+        HIP_TRY(sda::launch_mod_canonical(partial[0], D, res, m, h->stream));
+    }
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipMemcpyAsync(out_host, res, D * 8, hipMemcpyDeviceToHost, h->stream));
+    for (size_t g = 0; g < parts; ++g) HIP_TRY(hipStreamSynchronize(dev_of(h, g)->stream));
+    return SDA_OK;
+}
+
+// additive.rs:32-51 per column (batched.rs:19-53 with input_size 1): columns split over the devices;
+// out [n][D] clerk-major
+sda_status host_additive_generate(sda_engine* h, int64_t m, uint64_t n, const int64_t* secrets, uint64_t D,
+                                  const int64_t* draws, int64_t* out) {
+    const size_t G = n_devices(h);
+    return for_devices(h, [&](size_t g) -> sda_status {
+        uint64_t lo, w;
+        column_slice(D, g, G, &lo, &w);
+        if (w == 0) return SDA_OK;
+        sda_engine* d = dev_of(h, g);
+        HIP_TRY(hipSetDevice(d->device));
+        DevArena a;
+        if (sda_status e = stage(d, rup(w * 8) + rup(w * (n - 1) * 8 + 8) + rup(n * w * 8), &a)) return e;
+        int64_t* dsec = a.take<int64_t>(w);
+        int64_t* ddr = a.take<int64_t>(w * (n - 1) + 1);
+        int64_t* dout = a.take<int64_t>(n * w);
+        HIP_TRY(hipMemcpyAsync(dsec, secrets + lo, w * 8, hipMemcpyHostToDevice, d->stream));
+        if (n > 1)
+            HIP_TRY(hipMemcpyAsync(ddr, draws + lo * (n - 1), w * (n - 1) * 8, hipMemcpyHostToDevice, d->stream));
+        HIP_TRY(sda::launch_additive_generate(dsec, w, ddr, n, dout, m, d->stream));
+        HIP_TRY(hipMemcpy2DAsync(out + lo, D * 8, dout, w * 8, w * 8, n, hipMemcpyDeviceToHost, d->stream));
+        HIP_TRY(hipStreamSynchronize(d->stream));
+        return SDA_OK;
+    });
+}
+
+// packed_shamir.rs:40-43 per batch (batched.rs:19-53): batches split over the devices; out [n][B]
+sda_status host_packed_generate(sda_engine* h, const sda_sharing_scheme* s, const int64_t* secrets, uint64_t D,
+                                const int64_t* draws, int64_t* out) {
+    const uint64_t k = s->secret_count, t = s->privacy_threshold, n = s->share_count, B = (D + k - 1) / k;
+    const size_t G = n_devices(h);
+    return for_devices(h, [&](size_t g) -> sda_status {
+        uint64_t b0, nb;
+        shard(B, g, G, &b0, &nb);
+        if (nb == 0) return SDA_OK;
+        sda_engine* d = dev_of(h, g);
+        HIP_TRY(hipSetDevice(d->device));
+        const uint64_t s0 = b0 * k, ds = std::min(D, (b0 + nb) * k) - s0;   // the last batch may be short (padded)
+        DevArena a;
+        if (sda_status e = stage(d, rup(ds * 8) + rup(nb * t * 8 + 8) + rup(n * nb * 8), &a)) return e;
+        int64_t* dsec = a.take<int64_t>(ds);
+        int64_t* ddr = a.take<int64_t>(nb * t + 1);
+        int64_t* dout = a.take<int64_t>(n * nb);
+        HIP_TRY(hipMemcpyAsync(dsec, secrets + s0, ds * 8, hipMemcpyHostToDevice, d->stream));
+        if (t) HIP_TRY(hipMemcpyAsync(ddr, draws + b0 * t, nb * t * 8, hipMemcpyHostToDevice, d->stream));
+        if (sda_status e = ensure(&d->gen_log, &d->gen_log_bytes, sda::packed_gen_log_bytes())) return e;
+        sda::PackedGenArgs ga{dsec, ds, 1, ddr, dout};
+        HIP_TRY(sda::launch_packed_generate(ga, (uint32_t)k, (uint32_t)t, (uint32_t)n, (uint32_t)s->modulus,
+                                            (uint32_t)s->omega_secrets, (uint32_t)s->omega_shares, d->gen_tab,
+                                            d->gen_log, d->stream));
+        HIP_TRY(hipMemcpy2DAsync(out + b0, B * 8, dout, nb * 8, nb * 8, n, hipMemcpyDeviceToHost, d->stream));
+        HIP_TRY(hipStreamSynchronize(d->stream));
+        return SDA_OK;
+    });
+}
+
+// packed_shamir.rs:73-77 per batch (batched.rs:69-97), exact: batches split over the devices; out [dimension]
+sda_status host_packed_reconstruct(sda_engine* h, const sda_sharing_scheme* s, uint64_t dimension,
+                                   const uint64_t* indices, const int64_t* const* rows, uint64_t n_rows, int64_t* out) {
+    const uint64_t k = s->secret_count, B = (dimension + k - 1) / k;
+    const size_t G = n_devices(h);
+    return for_devices(h, [&](size_t g) -> sda_status {
+        uint64_t b0, nb;
+        shard(B, g, G, &b0, &nb);
+        if (nb == 0) return SDA_OK;
+        sda_engine* d = dev_of(h, g);
+        HIP_TRY(hipSetDevice(d->device));
+        const uint64_t s0 = b0 * k, ds = std::min(dimension, (b0 + nb) * k) - s0;
+        DevArena a;
+        if (sda_status e = stage(d, rup(n_rows * nb * 8) + rup(ds * 8), &a)) return e;
+        int64_t* din = a.take<int64_t>(n_rows * nb);
+        int64_t* dout = a.take<int64_t>(ds);
+        for (uint64_t i = 0; i < n_rows; ++i)        // batched.rs:83-85: clerk i's batches [b0, b0 + nb)
+            HIP_TRY(hipMemcpyAsync(din + i * nb, rows[i] + b0, nb * 8, hipMemcpyHostToDevice, d->stream));
+        if (sda_status e = ensure(&d->gen_log, &d->gen_log_bytes, sda::packed_gen_log_bytes())) return e;
+        sda::PackedRevealArgs ra{din, ds, 1, dout};
+        HIP_TRY(sda::launch_packed_reveal(ra, indices, (uint32_t)n_rows, (uint32_t)k, (uint32_t)s->modulus,
+                                          (uint32_t)s->omega_secrets, (uint32_t)s->omega_shares, SDA_REVEAL_EXACT,
+                                          d->rev_tab, d->gen_log, d->stream));
+        HIP_TRY(hipMemcpyAsync(out + s0, dout, ds * 8, hipMemcpyDeviceToHost, d->stream));
+        HIP_TRY(hipStreamSynchronize(d->stream));
+        return SDA_OK;
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+sda_status sda_engine_create_multi(const int* ordinals, int n_devices_, sda_engine** out) {
+    SDA_ENTRY;
+    if (!out) return fail(SDA_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    if (!ordinals || n_devices_ < 1 || n_devices_ > 64)
+        return fail(SDA_ERR_INVALID_ARGUMENT, "need 1..64 device ordinals");
+    sda_engine* h = nullptr;
+    if (sda_status e = sda_engine_create(ordinals[0], &h)) return e;
+    if (n_devices_ == 1) {                       // a one-device handle that still reduces through RCCL
+        h->sub.push_back(h);
+        *out = h;
+        return ok();
+    }
+    h->sub.push_back(h);
+    for (int g = 1; g < n_devices_; ++g) {
+        sda_engine* d = nullptr;
+        if (sda_status e = sda_engine_create(ordinals[g], &d)) {
+            const std::string msg = g_last_error;
+            sda_engine_destroy(h);
+            return fail(e, "device %d: %s", ordinals[g], msg.c_str());
+        }
+        h->sub.push_back(d);
+    }
+    HIP_TRY(hipSetDevice(h->device));
+    *out = h;
+    return ok();
+}
+
+int sda_engine_device_count(const sda_engine* h) { return h ? (int)n_devices(h) : 0; }
 
 }  // extern "C"

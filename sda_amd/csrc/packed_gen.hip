@@ -298,11 +298,14 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         {
             const uint32_t es = lb * k - 1;                                    // + i,      i <= k
             const uint32_t ed = (uint32_t)BS * k + lb * t - 1 - k;             // + i,      i >  k
-            // (lanes past B read whatever the LDS holds: they log nothing and store nothing)
+            // (lanes past B read whatever the LDS holds: they log nothing, store nothing and count as in range)
             static_for<1, L>([&](auto i) { raw[i] = lds[lpos(((uint32_t)i <= k ? es : ed) + i)]; });
         }
         bool in_range = true;
         static_for<1, L>([&](auto i) { in_range = in_range && ((uint64_t)(raw[i] + (P - 1)) < (uint64_t)(2 * P - 1)); });
+        // a dead lane's stale LDS words must not send its live partner to the fix-up kernel: it counts as in
+        // range, so how much fix-up work runs depends only on the inputs
+        in_range = in_range || !live;
         // A store pair (see the lane map above) takes the fast path only when both of its batches
         // are in range; otherwise both lanes log their batch for the generic exact fix-up kernel
         // (rare: raw i64 secrets) and the fast path below stores nothing for the pair.  (A call

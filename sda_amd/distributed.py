@@ -119,6 +119,10 @@ _WORK = {}
 # partial buffer -> generation of the last pass 1 written into it (a deferred ticket's pass-1 result is
 # still there only if no later split wrote the same buffer)
 _GEN = {}
+# out buffer -> generation of the last split that queued its result into it: a deferred ticket whose job
+# turns out signed rewrites `out` in finish(), which would clobber a LATER job's result in the same buffer
+# (never cleared: a dropped entry would fail a ticket still in flight; the keys are the allocator's addresses)
+_OUT_GEN = {}
 
 
 def _workspace(t, dim: int, st):
@@ -139,12 +143,16 @@ class SplitTicket:
     all-reduced flags into pinned host memory.  finish() waits for that 16-byte copy only, then:
     risk flag -> ValueError; negative flag -> the exact two-pass split, which rewrites `out`.
     `out` holds the job's result once finish() has returned.  Every rank must call finish() (the signed
-    path runs collectives), in the same order relative to its other collectives.  Idempotent."""
+    path runs collectives), in the same order relative to its other collectives.  Idempotent.
+    Until finish() returns, the job's share rows must stay as they are (the signed path reads them again)
+    and `out` must not be handed to another split: finish() raises ValueError for a signed job whose `out`
+    a later split has reused (its exact result would overwrite the later job's); a reused `partial` only
+    costs a recomputed pass 1."""
 
     def __init__(self, engine, modulus, tiles, dim, row_stride, partial, out, group, st, stats, flags_h, event,
-                 gen):
+                 gen, out_gen):
         self._args = (engine, modulus, tiles, dim, row_stride, partial, out, group, st, stats)
-        self._flags_h, self._event, self._gen = flags_h, event, gen
+        self._flags_h, self._event, self._gen, self._out_gen = flags_h, event, gen, out_gen
         self._finished = False
 
     def done(self) -> bool:
@@ -162,6 +170,10 @@ class SplitTicket:
             raise ValueError("participation split: an input lies outside [-(2^63 - m), 2^63 - m], where the "
                              "reference's running sum may wrap; combine on one rank or split by columns")
         if neg:
+            if _OUT_GEN.get(self._args[6].data_ptr()) != self._out_gen:
+                raise ValueError("participation split: this signed job's `out` was reused by a later split before "
+                                 "finish(); its exact result would overwrite that job's (one `out` per ticket in "
+                                 "flight)")
             _two_pass(*self._args, redo=_GEN.get(self._args[5].data_ptr()) != self._gen)
 
 
@@ -233,6 +245,7 @@ def _combine_split(engine, modulus: int, tiles, dim: int, row_stride: int, parti
         if len(_GEN) > 1024:
             _GEN.clear()
         gen = _GEN[partial.data_ptr()] = _GEN.get(partial.data_ptr(), 0) + 1
+        out_gen = _OUT_GEN[out.data_ptr()] = _OUT_GEN.get(out.data_ptr(), 0) + 1
         work[:dim].copy_(partial)
         dist.all_reduce(work, op=dist.ReduceOp.SUM, group=group)
         # the finalize is the result whenever no rank saw a negative input: queue it now, read the
@@ -246,7 +259,7 @@ def _combine_split(engine, modulus: int, tiles, dim: int, row_stride: int, parti
         else:                                    # host tensors (CPU / gloo tests): already there
             flags_h, event = work[dim:].clone(), None
     ticket = SplitTicket(engine, modulus, tiles, dim, row_stride, partial, out, group, st, stats, flags_h, event,
-                         gen)
+                         gen, out_gen)
     if defer:
         return ticket
     ticket.finish()

@@ -55,6 +55,8 @@ SIGNATURES = [
     ("sda_abi_version", C.c_int, []),
     ("sda_engine_create", _st, [C.c_int, C.POINTER(_vp)]),
     ("sda_engine_destroy", None, [_vp]),
+    ("sda_engine_create_multi", _st, [C.POINTER(C.c_int), C.c_int, C.POINTER(_vp)]),
+    ("sda_engine_device_count", C.c_int, [_vp]),
     ("sda_engine_synchronize", _st, [_vp]),
     ("sda_last_error_message", C.c_char_p, []),
     ("sda_status_string", C.c_char_p, [C.c_int]),
@@ -96,6 +98,8 @@ SIGNATURES = [
     ("sda_synth_fill_dev", _st, [_vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int64, C.c_int64, _vp]),
     ("sda_hbm_alloc", _st, [C.c_int, C.c_uint64, C.POINTER(_vp)]),
     ("sda_hbm_free", _st, [_vp]),
+    ("sda_hbm_trim", _st, [C.c_int, C.c_uint64]),
+    ("sda_hbm_stats", _st, [C.c_int, _u64p, _u64p, _u64p]),
     ("sda_varint_encode", _st, [_vp, _i64p, C.c_uint64, _u8p, C.c_uint64, _u64p]),
     ("sda_varint_decode", _st, [_vp, _u8p, C.c_uint64, _i64p, C.c_uint64, _u64p]),
     ("sda_clerk_decode_combine", _st, [_vp, C.POINTER(S.SharingSchemeC), C.POINTER(_u8p), _u64p, C.c_uint64,
@@ -185,15 +189,19 @@ class _HbmBlock:
                                          "version": 2, "strides": None}
 
     def __del__(self):
-        if getattr(self, "ptr", None):
+        # sda_hbm_free does not wait for the device (the buffer is only pooled); at interpreter shutdown the
+        # HIP runtime may already be gone, and the process exit releases everything anyway
+        if getattr(self, "ptr", None) and not sys.is_finalizing():
             self.lib.sda_hbm_free(self.ptr)
-            self.ptr = None
+        self.ptr = None
 
 
 class Engine:
-    """One engine handle = one HIP device + one stream (sda_engine_create)."""
+    """One engine handle = one HIP device + one stream (sda_engine_create), or, with `devices`, one handle over
+    several devices (sda_engine_create_multi): the host trait calls then split over them; the `_dev` entry points
+    run on devices[0]."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices: Optional[Sequence[int]] = None):
         # torch (when the caller uses it) ships its own HIP runtime; it has to open the device before
         # the engine's ROCm runtime does, or torch later reports "No HIP GPUs are available"
         t = sys.modules.get("torch")
@@ -201,9 +209,18 @@ class Engine:
             t.cuda.init()
         self.lib = load_library()
         h = _vp()
-        _check(self.lib.sda_engine_create(device, C.byref(h)))
+        if devices is None:
+            _check(self.lib.sda_engine_create(device, C.byref(h)))
+        else:
+            devs = (C.c_int * max(len(devices), 1))(*devices)
+            _check(self.lib.sda_engine_create_multi(devs, len(devices), C.byref(h)))
+            device = int(devices[0])
         self.h = h
         self.device = device
+
+    def device_count(self) -> int:
+        """Devices the handle's host calls use (sda_engine_device_count)."""
+        return int(self.lib.sda_engine_device_count(self.h))
 
     def close(self):
         if getattr(self, "h", None):
@@ -345,6 +362,16 @@ class Engine:
         nbytes = max(count * torch.empty((), dtype=dtype).element_size(), 1)
         return torch.as_tensor(_HbmBlock(self.lib, self.device, shape, dtype, nbytes),
                                device=torch.device("cuda", self.device))
+
+    def hbm_trim(self, keep_bytes: int = 0):
+        """Release this device's pooled sda_hbm_alloc buffers down to keep_bytes (sda_hbm_trim)."""
+        _check(self.lib.sda_hbm_trim(self.device, keep_bytes))
+
+    def hbm_stats(self):
+        """(live, pooled, retired) bytes of this device's sda_hbm_alloc buffers (sda_hbm_stats)."""
+        v = [C.c_uint64() for _ in range(3)]
+        _check(self.lib.sda_hbm_stats(self.device, *[C.byref(x) for x in v]))
+        return tuple(int(x.value) for x in v)
 
     # ---------------- device-resident entry points (raw device pointers, hipStream_t) ----------------
     def combine_dev(self, modulus, shares_ptr, n, dim, row_stride, out_ptr, stream=None):

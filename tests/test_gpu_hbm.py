@@ -1,7 +1,9 @@
 """sda_hbm_alloc / sda_hbm_free (include/sda_engine.h) and Engine.hbm_empty on the GPU: the buffer is usable
 by torch and by the engine's kernels, share-gen into it is bit-identical to share-gen into a torch buffer, it
-returns to the pool with its tensor and is handed out again, and the error behaviour is the header's."""
+returns to the pool with its tensor and is handed out again, the pool is bounded and trimmed (physical chunks
+released, the virtual range retired), and the error behaviour is the header's."""
 import ctypes as C
+import os
 
 import pytest
 
@@ -44,7 +46,8 @@ def test_hbm_tensor_torch_and_engine(engine):
     ptr = a.data_ptr()
     del a                                                      # back to the pool with its tensor, still mapped
     a2 = engine.hbm_empty((rows, cols))
-    assert a2.data_ptr() == ptr                                # the pooled buffer is handed out again
+    if os.environ.get("SDA_HBM_POOL_MB", "") != "0":          # (the r04y repro runs with the pool disabled)
+        assert a2.data_ptr() == ptr                            # the pooled buffer is handed out again
     a2.fill_(-1)
     assert int(a2.min()) == -1 and int(a2.max()) == -1
 
@@ -74,3 +77,74 @@ def test_packed_generate_into_hbm_matches_torch_buffer(engine):
                 f"{hex(sh_t.data_ptr())} {hex(sec.data_ptr())} {hex(drw.data_ptr())}")
         if mode == E.REVEAL_CANONICAL:
             assert int(sh_h.min()) >= 0 and int(sh_h.max()) < p
+
+
+def test_hbm_trim_realloc_sequence_matches_torch(engine, monkeypatch):
+    """The sequence that corrupted data in round 4 (profiles/r04y): a buffer is freed and unmapped, torch takes
+    fresh memory, new buffers are allocated and share-gen writes one of them -- now with every free trimmed
+    (SDA_HBM_POOL_MB=0).  Share-gen into the new buffer equals share-gen into a torch buffer, repeated reads
+    agree, and the torch block allocated in between is untouched (HBM backing)."""
+    import torch
+    monkeypatch.setenv("SDA_HBM_POOL_MB", "0")
+    st = torch.cuda.current_stream().cuda_stream
+    dev = torch.device("cuda", engine.device)
+    sch = S.CONFIG_PACKED
+    p, k, t, n = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count
+    V, Dm = 40, 1_000_000
+    B = Dm // k
+    _, _, retired0 = engine.hbm_stats()
+    for r in range(3):
+        a = engine.hbm_empty((300, 1 << 20))                   # 2.4 GB, as the earlier test's buffer
+        engine.synth_fill_dev(a.data_ptr(), 300, 1 << 20, 40 + r, 1, 1 << 40, st)
+        torch.cuda.synchronize()
+        a_lo, a_hi = a.data_ptr(), a.data_ptr() + a.numel() * 8
+        del a
+        engine.hbm_trim(0)
+        assert engine.hbm_stats()[1] == 0
+        torch.cuda.empty_cache()
+        blk = torch.full((300, 1 << 20), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device=dev)
+        sec = engine.hbm_empty((V, Dm))
+        engine.synth_fill_dev(sec.data_ptr(), V, Dm, 21 + r, 0, p, st)
+        drw = engine.hbm_empty((V, B, t))
+        engine.synth_fill_dev(drw.data_ptr(), V * B, t, 22 + r, 0, p - 1, st)
+        sh_h = engine.hbm_empty((V, n, B))
+        for buf in (sec, drw, sh_h):                           # a retired range is never mapped again
+            assert buf.data_ptr() + buf.numel() * 8 <= a_lo or buf.data_ptr() >= a_hi
+        sh_t = torch.empty((V, n, B), dtype=torch.int64, device=dev)
+        for sh in (sh_h, sh_t):
+            engine.packed_generate_mode_dev(sch, sec.data_ptr(), Dm, V, drw.data_ptr(), sh.data_ptr(),
+                                            E.REVEAL_EXACT, st)
+        torch.cuda.synchronize()
+        for _ in range(2):
+            assert torch.equal(sh_h, sh_t)
+            assert int((sh_h == 0).sum()) == int((sh_t == 0).sum())
+        assert int((blk != 0x5A5A5A5A5A5A5A5A).sum()) == 0
+        del sec, drw, sh_h, sh_t, blk
+    engine.hbm_trim(0)
+    live, pooled, retired = engine.hbm_stats()
+    assert pooled == 0 and retired > retired0
+
+
+def test_hbm_pool_is_bounded(engine, monkeypatch):
+    """Freed buffers beyond SDA_HBM_POOL_MB are trimmed (oldest first) at the next allocation; a pooled buffer
+    is handed out again while it fits the bound; sda_hbm_trim empties the pool."""
+    import torch
+    engine.hbm_trim(0)
+    monkeypatch.setenv("SDA_HBM_POOL_MB", "256")
+    bufs = [engine.hbm_empty((16 << 20,)) for _ in range(4)]    # 4 x 128 MiB
+    ptrs = [b.data_ptr() for b in bufs]
+    for i in range(4):                                         # freed in order: bufs[0] is the oldest
+        bufs[i] = None
+    live, pooled, _ = engine.hbm_stats()
+    assert pooled >= 4 * (128 << 20)                           # free only pools (no wait, no trim)
+    x = engine.hbm_empty((16 << 20,))                          # trims to 256 MiB, then reuses a pooled buffer
+    assert x.data_ptr() in ptrs[2:]                            # the two oldest were trimmed
+    live, pooled, _ = engine.hbm_stats()
+    assert pooled <= 256 << 20
+    x.fill_(7)
+    assert int(x.sum()) == 7 * x.numel()
+    del x
+    engine.hbm_trim(0)
+    assert engine.hbm_stats()[1] == 0
+    with pytest.raises(SdaError):
+        E._check(engine.lib.sda_hbm_trim(-1, 0))

@@ -171,3 +171,74 @@ def test_recipient_reveal_wide_scheme(engine):
         mo = be.secret_reconstruct(ss, D, indexed)
         exp = be.positive(m, be.secret_unmask(ms, (be.mask_combine(ms, tr.masks), mo)))
         assert_same(got, exp, "wide")
+
+
+def _signed_clerk_results(ss, D, seed):
+    """Arbitrary signed clerk results in (-p, p) for every clerk: the reveal interpolates whatever it gets."""
+    p, n = ss.prime_modulus, ss.share_count
+    B = (D + ss.secret_count - 1) // ss.secret_count
+    rng = np.random.default_rng(seed)
+    return [rng.integers(-(p - 1), p, size=B, dtype=np.int64) for _ in range(n)]
+
+
+def _stepwise(ms, masks, ss, D, indexed, m):
+    be = OracleBackend()
+    mo = be.secret_reconstruct(ss, D, indexed)                # tss' exact signed representatives
+    mask = be.mask_combine(ms, masks) if ms.has_mask() else np.zeros(0, np.int64)
+    return be.positive(m, be.secret_unmask(ms, (mask, mo))), mo, mask
+
+
+@pytest.mark.parametrize("ms_kind", ["none", "full", "chacha"])
+def test_recipient_residue_only_runs_canonical_identically(engine, monkeypatch, ms_kind):
+    """Masking modulus (or no mask) == output modulus == p: the pipeline runs the canonical reveal for an EXACT
+    request.  On signed clerk results its output equals the step-wise oracle flow over tss'
+    exact reveal, and the forced-EXACT pipeline (SDA_RECIPIENT_EXACT=1), byte for byte."""
+    ss = S.CONFIG_PACKED
+    D = 8 * 523 + 5
+    ms = {"none": S.NoMasking(), "full": S.FullMasking(P), "chacha": S.ChaChaMasking(P, D, 128)}[ms_kind]
+    rng = Draws(0x77)
+    masks = [] if ms_kind == "none" else ([rng.below(P, D) for _ in range(3)] if ms_kind == "full"
+                                          else [rng.u32(4) for _ in range(3)])
+    res = _signed_clerk_results(ss, D, 3)
+    indexed = [(c, res[c]) for c in (25, 3, 17, 8, 0, 11, 20, 6, 14, 1, 22, 9, 5, 19, 12, 24)]
+    exp, _, _ = _stepwise(ms, masks, ss, D, indexed, P)
+    got = engine.recipient_reveal(ms, masks, ss, D, indexed, P)
+    monkeypatch.setenv("SDA_RECIPIENT_EXACT", "1")
+    forced = engine.recipient_reveal(ms, masks, ss, D, indexed, P)
+    assert_same(got, exp, ms_kind)
+    assert_same(forced, exp, ms_kind + " forced exact")
+
+
+@pytest.mark.parametrize("which", ["mask_modulus", "output_modulus"])
+def test_recipient_keeps_exact_when_moduli_differ(engine, which):
+    """A masking modulus or output modulus other than p makes the output depend on the reveal's signed
+    representative, so the pipeline keeps tss' exact reveal: the output equals the exact step-wise flow and
+    differs from what a canonical reveal would give on some elements."""
+    ss = S.CONFIG_PACKED
+    D = 8 * 301 + 1
+    q = P + 2 if which == "mask_modulus" else P
+    m_out = P if which == "mask_modulus" else 1 << 40
+    ms = S.FullMasking(q)
+    rng = Draws(0x78)
+    masks = [rng.below(q, D) for _ in range(2)]
+    res = _signed_clerk_results(ss, D, 4)
+    indexed = [(c, res[c]) for c in range(ss.reconstruction_threshold())]
+    exp, mo, mask = _stepwise(ms, masks, ss, D, indexed, m_out)
+    be = OracleBackend()
+    canon = be.positive(m_out, be.secret_unmask(ms, (mask, np.mod(mo, P))))
+    assert (np.asarray(canon) != np.asarray(exp)).any()      # the representative matters here
+    got = engine.recipient_reveal(ms, masks, ss, D, indexed, m_out)
+    assert_same(got, exp, which)
+
+
+def test_recipient_duplicate_points_fall_back_to_exact(engine):
+    """Equal moduli but a repeated clerk index (no Lagrange form): the pipeline falls back to the exact reveal
+    and matches the step-wise flow (tss' Newton over the repeated point)."""
+    ss = S.FULL_LOOP_PACKED
+    p = ss.prime_modulus
+    D = 3 * 5
+    res = _signed_clerk_results(ss, D, 5)
+    indexed = [(c, res[c]) for c in (0, 1, 2, 3, 4, 5, 2)]
+    exp, _, _ = _stepwise(S.NoMasking(), [], ss, D, indexed, p)
+    got = engine.recipient_reveal(S.NoMasking(), [], ss, D, indexed, p)
+    assert_same(got, exp, "duplicate points")

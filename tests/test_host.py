@@ -117,6 +117,22 @@ def _worker_rows(rank, world, port, q):
         t.finish()                                   # idempotent
     res["deferred"] = [(o.tolist(), O.combine(m, x).tolist(), s.signed, s.redo_pass1, s.passes)
                        for o, x, s in zip(outs, jobs, stats)]
+    # a signed deferred job whose `out` a later split reuses before finish(): refused with ValueError on
+    # every rank (never the earlier job's exact result written over the later job's); the later job is intact
+    x_s, x_n = jobs[1], jobs[0]
+    start, count = Dd.shard_range(x_s.shape[0], rank, world)
+    ms_, mn_ = (torch.from_numpy(v[start:start + count].copy()) for v in (x_s, x_n))
+    shared_out = torch.empty(D, dtype=torch.int64)
+    part2 = torch.empty(D, dtype=torch.int64)
+    t_s = Dd.combine_rows_sharded(CpuEngine(), m, ms_.data_ptr(), count, D, D, part, shared_out, defer=True)
+    t_n = Dd.combine_rows_sharded(CpuEngine(), m, mn_.data_ptr(), count, D, D, part2, shared_out, defer=True)
+    try:
+        t_s.finish()
+        res["out_reuse_refused"] = False
+    except ValueError:
+        res["out_reuse_refused"] = True
+    t_n.finish()
+    res["out_reuse_later_intact"] = shared_out.tolist() == O.combine(m, x_n).tolist()
     # an input the reference's running sum could wrap on: the split refuses it (never a wrong value)
     m = 1000003
     x = torch.from_numpy(synth.fill(4, 8, 1, 0, 100))
@@ -141,6 +157,8 @@ def test_gloo_sharded_combine_matches_single_pass(world):
     inputs where the reference's own sum may wrap."""
     res = _run_world2(_worker_rows, world)
     assert res.pop("wrap_refused") is True
+    assert res.pop("out_reuse_refused") is True
+    assert res.pop("out_reuse_later_intact") is True
     deferred = res.pop("deferred")
     for got, exp, *_ in deferred:
         assert got == exp
