@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--chacha-seeds", type=int, default=256)
     ap.add_argument("--no-side", action="store_true", help="skip packed-Shamir / ChaCha legs")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the host-path leg (sda_share_combine from host rows at the headline size)")
+    ap.add_argument("--host-calls", type=int, default=2, help="timed sda_share_combine calls in the host-path leg")
     ap.add_argument("--no-signed-split", action="store_true",
                     help="N > 1: skip the signed-shares leg of the participation split (two-pass path)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -203,6 +206,60 @@ def cpu_baseline_chacha(threads: int, budget_s: float):
             "all_cores": round(threads * per * D / ta, 1), "cores": threads,
             "sample": f"{per} seeds x 1M-dim on 1 core, {threads * per} on {threads} threads; median of {n1}/{na} "
                       "runs; oracle/sda_oracle.c at -O2"}
+
+
+def host_path_leg(args, torch, eng, shares, dev_out, N, D, m, dev):
+    """The drop-in boundary at the headline size: ShareCombiner::combine (clerk.rs:85-86 -> combiner.rs:16-28)
+    through the HOST entry point the Rust shim calls, sda_share_combine, over the same N x D i64 rows held in
+    host memory as N separate row buffers (a Vec<Vec<i64>>).  The engine streams them through pinned double
+    buffers in row tiles (engine.cpp, host path), so the call is bound by the host -> device link; the leg
+    reports it beside the measured pinned and pageable H2D rates of the same box.  Bit-exact check: the call's
+    result equals the device-resident combine of the same rows (the headline's last step)."""
+    from sda_amd import schemes as S
+    t0 = time.perf_counter()
+    host = torch.empty((N, D), dtype=torch.int64)          # pageable host memory, like the Rust Vecs
+    host.copy_(shares)
+    torch.cuda.synchronize()
+    fill_s = time.perf_counter() - t0
+    hn = host.numpy()
+    rows = [hn[i] for i in range(N)]
+    sch = S.Additive(3, m)
+    times = []
+    got = None
+    for i in range(1 + max(1, args.host_calls)):
+        t0 = time.perf_counter()
+        got = eng.share_combine(sch, rows)
+        if i:
+            times.append(time.perf_counter() - t0)
+    ok = bool(np.array_equal(got, dev_out.cpu().numpy()))
+    if not ok:
+        raise SystemExit("host-path combine check FAILED")
+    # the link's own rates on this box: 1 GiB pinned and pageable host buffers -> HBM
+    def h2d(pinned):
+        src = torch.empty(1 << 27, dtype=torch.int64, pin_memory=pinned)
+        src.fill_(1)
+        dst = torch.empty(1 << 27, dtype=torch.int64, device=dev)
+        dst.copy_(src, non_blocking=pinned)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            dst.copy_(src, non_blocking=pinned)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return 8.0 * (1 << 27) / statistics.median(ts) / 1e9
+    pinned_gbps, pageable_gbps = h2d(True), h2d(False)
+    t = statistics.median(times)
+    gbps = 8.0 * N * D / t / 1e9
+    del host, hn, rows
+    return {"config": f"sda_share_combine (host entry point) over {N:,} host rows x {D:,} i64 (the headline job)",
+            "ms_per_call": round(t * 1e3, 1), "GBps": round(gbps, 2), "calls": len(times),
+            "h2d_pinned_GBps": round(pinned_gbps, 2), "h2d_pageable_GBps": round(pageable_gbps, 2),
+            "frac_of_pinned_h2d": round(gbps / pinned_gbps, 4),
+            "stage_mb": int(os.environ.get("SDA_HOST_STAGE_MB", "256")),
+            "host_threads": int(os.environ.get("SDA_HOST_THREADS", "0")) or min(os.cpu_count() or 1, 16),
+            "host_fill_s": round(fill_s, 2),
+            "check": "bit-exact: equals the device-resident combine of the same rows, all columns"}
 
 
 class TimedEngine:
@@ -488,6 +545,9 @@ def main():
                 "passes": sst.passes,
                 "check": "bit-exact on 256 sampled columns: the reference recurrence over all ranks' rows in order"}
             log(f"[combine_signed_split] {json.dumps(side['combine_signed_split'])}")
+        if not args.no_host_path and world == 1 and not tile and args.only is None:
+            side["host_path"] = host_path_leg(args, torch, eng, shares, out, N, D, m, dev)
+            log(f"[host_path] {json.dumps(side['host_path'])}")
         del shares
         torch.cuda.empty_cache()         # the next leg gets fresh allocations, not a reused segment
 
@@ -790,6 +850,7 @@ def main():
         return
     if rank == 0:
         traffic = traffic_from_profile(tile if tile else N, D)
+        tr = roofline_trace(traffic[2], bytes_per_launch, kernel_ms)
         rec = {
             "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
@@ -807,7 +868,8 @@ def main():
                        "buffers": "torch.empty"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic[0], "traffic_source": traffic[1]},
+                         "traffic": traffic[0], "traffic_source": traffic[1],
+                         **({"trace": tr} if tr else {})},
             "kernel_ms": round(kernel_ms, 4),
             "kernel_bytes_per_launch": bytes_per_launch,
         }
@@ -967,18 +1029,37 @@ def valu_roofline(key, ms, waves, blocks=None):
 
 
 def traffic_from_profile(N, D):
-    """(HBM bytes per combine launch, the profiles/ session they come from) from the committed rocprofv3
-    PMC pass, if it was collected for this exact workload; FETCH_SIZE doubled per MI355X_MICROARCH.md
-    §HBM.  (None, None) otherwise."""
+    """(HBM bytes per combine launch, the profiles/ session they come from, that session's trace record) from
+    the committed rocprofv3 PMC pass, if it was collected for this exact workload; FETCH_SIZE doubled per
+    MI355X_MICROARCH.md §HBM.  (None, None, None) otherwise."""
     path = os.path.join(ROOT, "profiles", "combine_traffic.json")
     try:
         with open(path) as f:
             for t in json.load(f)["launches"]:
                 if t.get("rows") == N and t.get("dim") == D:
-                    return t["hbm_bytes_per_launch"], t.get("source")
+                    return t["hbm_bytes_per_launch"], t.get("source"), t.get("trace")
     except (OSError, ValueError, KeyError):
         pass
-    return None, None
+    return None, None, None
+
+
+def roofline_trace(trace, bytes_per_launch, kernel_ms):
+    """The dominant kernel as the committed profile session saw it, beside this run's live HIP-event figure:
+    that session's rocprofv3 kernel-trace average and the fraction it gives, and the same session's untraced
+    HIP-event kernel time, so a difference between this line and the profile splits into tracing overhead
+    (traced vs untraced on the profiled box) and box-to-box spread (untraced there vs live here)."""
+    if not trace or not trace.get("kernel_avg_ms"):
+        return None
+    avg = trace["kernel_avg_ms"]
+    r = {"session": trace.get("session"), "kernel_avg_ms": round(avg, 4),
+         "frac": round(bytes_per_launch / (avg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+         "dispatches": trace.get("dispatches")}
+    un = trace.get("untraced_bench_kernel_ms")
+    if un:
+        r["untraced_kernel_ms_same_box"] = round(un, 4)
+        r["tracing_overhead"] = round(avg / un - 1.0, 4)
+        r["live_vs_profiled_box"] = round(kernel_ms / un - 1.0, 4)
+    return r
 
 
 if __name__ == "__main__":

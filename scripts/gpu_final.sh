@@ -6,8 +6,10 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-final}
-bash scripts/gpu_steps.sh "$TAG" host tests smoke "bench:" "trace:--steps 10 --warmup 2 --no-cpu" \
+bash scripts/gpu_steps.sh "$TAG" host tests smoke "bench:" "trace:--steps 10 --warmup 2 --no-cpu --no-host-path" \
   "pmc:FETCH_SIZE:--only combine --steps 3 --warmup 1" "pmc:WRITE_SIZE:--only combine --steps 3 --warmup 1" \
   "sh:pmc_shamir.sh ${TAG}_shamir --only shamir --steps 3 --warmup 1" \
   "sh:pmc_shamir.sh ${TAG}_chacha --only chacha --steps 3 --warmup 1" \
-  "bench:--config 3 --steps 2 --warmup 1 --no-cpu" "bench:--config 4 --steps 1 --warmup 1 --no-cpu"
+  "bench:--config 3 --steps 2 --warmup 1 --no-cpu" "bench:--config 4 --steps 1 --warmup 1 --no-cpu" \
+  "pmc:FETCH_SIZE:--config 3 --only combine --steps 1 --warmup 0 --no-cpu" \
+  "pmc:WRITE_SIZE:--config 3 --only combine --steps 1 --warmup 0 --no-cpu"

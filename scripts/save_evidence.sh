@@ -21,6 +21,8 @@ cp "$S/bench_10.json" "$D/configs/config3.json"
 cp "$S/bench_10.log" "$D/configs/config3.log"
 cp "$S/bench_11.json" "$D/configs/config4.json"
 cp "$S/bench_11.log" "$D/configs/config4.log"
+cp "$S/pmc_12.txt" "$D/pmc_c3_fetch.txt" 2>/dev/null || true
+cp "$S/pmc_13.txt" "$D/pmc_c3_write.txt" 2>/dev/null || true
 python3 - "$TAG" <<'EOF'
 import json, re, sys
 tag = sys.argv[1]
@@ -28,16 +30,45 @@ def kib(path, ctr):
     txt = open(f"profiles/{tag}/{path}").read()
     m = re.search(r"combine_exact_kernel<long, 2, 8, true, false, false>\n\s+" + ctr + r"\s+([0-9.e+]+)", txt)
     return float(m.group(1))
+import csv
+def trace_avg_ms(grid_x):
+    # the dominant combine launch's average in this session's rocprofv3 --kernel-trace (kernel_stats_by_grid.csv)
+    for r in csv.DictReader(open(f"profiles/{tag}/kernel_stats_by_grid.csv")):
+        if r["kernel"].startswith("sda::combine_exact_kernel<long, 2, 8, true, false, false>") and \
+                int(r["grid_x"]) == grid_x:
+            return float(r["avg_us"]) / 1e3, int(r["calls"])
+    return None, 0
+untraced = json.load(open(f"profiles/{tag}/bench.json"))
+traced = json.load(open(f"profiles/{tag}/bench_traced.json"))
 fetch, write = kib("pmc_6.txt", "FETCH_SIZE"), kib("pmc_7.txt", "WRITE_SIZE")
 traffic = int(round((2 * fetch + write) * 1024))
+avg, calls = trace_avg_ms(500224)
 p = "profiles/combine_traffic.json"
 d = json.load(open(p))
 for l in d["launches"]:
     if l["rows"] == 10000 and l["dim"] == 1000000:
         l["hbm_bytes_per_launch"] = traffic
         l["source"] = f"profiles/{tag}/pmc_6.txt + pmc_7.txt (2 x FETCH_SIZE + WRITE_SIZE, KiB)"
+        l["trace"] = {"session": f"profiles/{tag}", "kernel_avg_ms": avg, "dispatches": calls,
+                      "traced_bench_kernel_ms": traced.get("kernel_ms"),
+                      "untraced_bench_kernel_ms": untraced.get("kernel_ms"),
+                      "untraced_ms_per_step": untraced.get("ms_per_step")}
+# configs[3]: the 1000-row x 10M accumulate launch (grid 5,000,224), its own FETCH / WRITE passes
+try:
+    f3, w3 = kib("pmc_c3_fetch.txt", "FETCH_SIZE"), kib("pmc_c3_write.txt", "WRITE_SIZE")
+    for l in d["launches"]:
+        if l["rows"] == 1000 and l["dim"] == 10000000:
+            l["hbm_bytes_per_launch"] = int(round((2 * f3 + w3) * 1024))
+            l["source"] = f"profiles/{tag}/pmc_c3_fetch.txt + pmc_c3_write.txt (2 x FETCH_SIZE + WRITE_SIZE, KiB)"
+            a3, c3 = trace_avg_ms(5000224)
+            c3j = json.load(open(f"profiles/{tag}/configs/config3.json"))
+            l["trace"] = {"session": f"profiles/{tag}", "kernel_avg_ms": a3, "dispatches": c3,
+                          "untraced_bench_kernel_ms": c3j.get("kernel_ms")}
+except (OSError, AttributeError) as e:
+    print("configs[3] traffic not updated:", e)
 json.dump(d, open(p, "w"), indent=1)
 print("combine traffic per launch:", traffic, "B =", traffic / (8 * (10000 * 1000000 + 1000000)), "x algorithmic")
+print("trace avg", avg, "ms over", calls, "dispatches; untraced bench kernel", untraced.get("kernel_ms"), "ms")
 EOF
 python3 scripts/kernel_report.py "$S/trace" "gpurun_out/pmc_${TAG}_shamir" "gpurun_out/pmc_${TAG}_chacha" \
   > "$D/kernel_report.json"

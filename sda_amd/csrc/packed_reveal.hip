@@ -32,15 +32,6 @@ struct FE {
     uint32_t c;
 };
 
-// SDA_REVEAL_NOMEM (build-time measurement variant, never shipped): bit 0 -- the shares come from a hash of
-// the batch address instead of HBM; bit 1 -- the secrets stay in LDS (no stores).  3 times the reveal's
-// arithmetic alone.  SDA_REVEAL_NT_FLUSH: the staged flush writes with non-temporal stores.
-#ifndef SDA_REVEAL_NOMEM
-#define SDA_REVEAL_NOMEM 0
-#endif
-#ifndef SDA_REVEAL_NT_FLUSH
-#define SDA_REVEAL_NT_FLUSH 0
-#endif
 // The k secrets of a batch are adjacent in `out` (batched.rs:94 appends batch after batch), so a
 // lane's own stores would stride by 8k bytes.  With STAGED the workgroup parks its results in
 // LDS ([lane][k]) and writes the nb*k block back with coalesced stores.
@@ -52,15 +43,7 @@ __device__ __forceinline__ void reveal_flush(int64_t* lds_o, int64_t* o, uint64_
         const uint64_t first = b0 * k;
         const uint64_t last = (b0 + 256 < B ? b0 + 256 : B) * k;
         const uint32_t cnt = (uint32_t)((last < D ? last : D) - first);
-        for (uint32_t j = threadIdx.x; j < cnt; j += 256) {
-            if constexpr (SDA_REVEAL_NOMEM & 2) {
-                if (lds_o[j] == INT64_MIN + 1) o[first + j] = 0;     // never: keeps the results live
-            } else if constexpr (SDA_REVEAL_NT_FLUSH) {
-                __builtin_nontemporal_store(lds_o[j], o + first + j);
-            } else {
-                o[first + j] = lds_o[j];
-            }
-        }
+        for (uint32_t j = threadIdx.x; j < cnt; j += 256) o[first + j] = lds_o[j];
     }
 }
 
@@ -74,14 +57,6 @@ __device__ __forceinline__ bool load_points(const int64_t* __restrict__ sh, uint
     const int64_t P = (int64_t)p;
     s[0] = FE{0, 0};
     bool in_range = true;
-    if constexpr (SDA_REVEAL_NOMEM & 1) {
-        const uint32_t h = (uint32_t)((uintptr_t)sh >> 3) * 0x9E3779B1u;
-        static_for<1, MMAX>([&](auto i) {
-            const int32_t x = (uint32_t)i < m ? (int32_t)((h + (uint32_t)i * 0x85EBCA77u) & 0x3FFFFFFFu) : 0;
-            s[i] = FE{x, (uint32_t)x};
-        });
-        return true;
-    }
     auto take = [&](auto i, int64_t v) {
         in_range = in_range && ((uint32_t)i >= m || (uint64_t)(v + (P - 1)) < (uint64_t)(2 * P - 1));
         const int32_t x = (uint32_t)i < m ? (int32_t)v : 0;
