@@ -208,14 +208,16 @@ def cpu_baseline_chacha(threads: int, budget_s: float):
                       "runs; oracle/sda_oracle.c at -O2"}
 
 
-def host_path_leg(args, torch, eng, shares, dev_out, N, D, m, dev):
+def host_path_leg(args, torch, eng, shares, N, D, m, dev, st):
     """The drop-in boundary at the headline size: ShareCombiner::combine (clerk.rs:85-86 -> combiner.rs:16-28)
     through the HOST entry point the Rust shim calls, sda_share_combine, over the same N x D i64 rows held in
     host memory as N separate row buffers (a Vec<Vec<i64>>).  The engine streams them through pinned double
     buffers in row tiles (engine.cpp, host path), so the call is bound by the host -> device link; the leg
     reports it beside the measured pinned and pageable H2D rates of the same box.  Bit-exact check: the call's
-    result equals the device-resident combine of the same rows (the headline's last step)."""
+    result equals the device-resident combine of the same rows (the buffer holds the signed leg's rows by now)."""
     from sda_amd import schemes as S
+    dev_out = torch.empty(D, dtype=torch.int64, device=dev)
+    eng.combine_dev(m, shares.data_ptr(), N, D, D, dev_out.data_ptr(), st)
     t0 = time.perf_counter()
     host = torch.empty((N, D), dtype=torch.int64)          # pageable host memory, like the Rust Vecs
     host.copy_(shares)
@@ -546,7 +548,7 @@ def main():
                 "check": "bit-exact on 256 sampled columns: the reference recurrence over all ranks' rows in order"}
             log(f"[combine_signed_split] {json.dumps(side['combine_signed_split'])}")
         if not args.no_host_path and world == 1 and not tile and args.only is None:
-            side["host_path"] = host_path_leg(args, torch, eng, shares, out, N, D, m, dev)
+            side["host_path"] = host_path_leg(args, torch, eng, shares, N, D, m, dev, stream())
             log(f"[host_path] {json.dumps(side['host_path'])}")
         del shares
         torch.cuda.empty_cache()         # the next leg gets fresh allocations, not a reused segment
