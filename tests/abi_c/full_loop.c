@@ -69,8 +69,26 @@ int main(void) {
     const uint64_t n = sda_scheme_output_size(&ss), B = sda_share_length(&ss, D);
     if (P > MAXP || n > MAXN || D > MAXV || n * B > MAXN * MAXV) return 2;
 
+    /* SDA_TEST_DEVICES="0,0,..." opens one handle over those ordinals (sda_engine_create_multi): the host
+     * trait calls then split over them (a one-device list reduces ChaCha masks through a one-rank RCCL
+     * communicator) */
     sda_engine* h = NULL;
-    check(sda_engine_create(0, &h), "sda_engine_create");
+    const char* devs = getenv("SDA_TEST_DEVICES");
+    if (devs && *devs) {
+        int ord[16], nd = 0;
+        for (const char* c = devs; *c && nd < 16;) {
+            ord[nd++] = atoi(c);
+            while (*c && *c != ',') ++c;
+            if (*c == ',') ++c;
+        }
+        check(sda_engine_create_multi(ord, nd, &h), "sda_engine_create_multi");
+        if (sda_engine_device_count(h) != nd) {
+            fprintf(stderr, "sda_engine_device_count: %d != %d\n", sda_engine_device_count(h), nd);
+            return 1;
+        }
+    } else {
+        check(sda_engine_create(0, &h), "sda_engine_create");
+    }
     printf("abi_version: %d\n", sda_abi_version());
 
     char key[64];

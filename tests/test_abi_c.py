@@ -51,7 +51,10 @@ def _parse(out):
     for line in out.splitlines():
         if ":" in line:
             k, v = line.split(":", 1)
-            res[k.strip()] = [int(x) for x in v.split()]
+            try:
+                res[k.strip()] = [int(x) for x in v.split()]
+            except ValueError:      # not one of the program's lines (RCCL prints its version banner at init)
+                continue
     return res
 
 
@@ -60,12 +63,16 @@ def _ensure_built():
         subprocess.run(["make", "-C", os.path.dirname(BIN)], check=True, capture_output=True)
 
 
+@pytest.mark.parametrize("devices", ["", "0", "0,0,0"], ids=["handle", "multi1", "multi3"])
 @pytest.mark.parametrize("variant", ["simple", "with_fullmask", "with_chachamask", "with_packedshamir"])
-def test_c_program_full_loop(variant):
+def test_c_program_full_loop(variant, devices):
+    """One device handle, a one-device multi handle (ChaCha through a one-rank RCCL communicator, RCCL loaded
+    from /opt/rocm in a process without torch) and a three-slice handle on one GPU (sda_engine_create_multi)."""
     with open(os.path.join(HERE, "golden", "full_loop_kat.json")) as f:
         v = json.load(f)[variant]
     _ensure_built()
     env = {k: val for k, val in os.environ.items() if not k.startswith("PYTHON")}
+    env["SDA_TEST_DEVICES"] = devices
     r = subprocess.run([BIN], input=_program_input(v), capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stderr
     got, t = _parse(r.stdout), v["trace"]
