@@ -26,9 +26,10 @@ cp "$S/pmc_13.txt" "$D/pmc_c3_write.txt" 2>/dev/null || true
 python3 - "$TAG" <<'EOF'
 import json, re, sys
 tag = sys.argv[1]
-def kib(path, ctr):
+def kib(path, ctr, acc="false"):
+    # acc: the accumulating instantiation (configs[3]'s row tiles) is <long, 2, 8, true, true, false>
     txt = open(f"profiles/{tag}/{path}").read()
-    m = re.search(r"combine_exact_kernel<long, 2, 8, true, false, false>\n\s+" + ctr + r"\s+([0-9.e+]+)", txt)
+    m = re.search(r"combine_exact_kernel<long, 2, 8, true, " + acc + r", false>\n\s+" + ctr + r"\s+([0-9.e+]+)", txt)
     return float(m.group(1))
 import csv
 def trace_avg_ms(grid_x):
@@ -55,7 +56,7 @@ for l in d["launches"]:
                       "untraced_ms_per_step": untraced.get("ms_per_step")}
 # configs[3]: the 1000-row x 10M accumulate launch (grid 5,000,224), its own FETCH / WRITE passes
 try:
-    f3, w3 = kib("pmc_c3_fetch.txt", "FETCH_SIZE"), kib("pmc_c3_write.txt", "WRITE_SIZE")
+    f3, w3 = kib("pmc_c3_fetch.txt", "FETCH_SIZE", "true"), kib("pmc_c3_write.txt", "WRITE_SIZE", "true")
     for l in d["launches"]:
         if l["rows"] == 1000 and l["dim"] == 10000000:
             l["hbm_bytes_per_launch"] = int(round((2 * f3 + w3) * 1024))

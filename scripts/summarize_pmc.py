@@ -15,4 +15,4 @@ for r in rows:
 for k, cs in acc.items():
     print(k)
     for c, v in sorted(cs.items()):
-        print(f"   {c:28s} {sum(v)/len(v):16.4g}   (n={len(v)})")
+        print(f"   {c:28s} {sum(v)/len(v):18.10g}   (n={len(v)})")
