@@ -731,6 +731,8 @@ def main():
                                              "the slots", "matrix": "count pass, decode to an int32 matrix, exact "
                                              "combine", "fused": "count pass, fused column-tile decode+combine"
                                     }.get(default_path, default_path),
+            "buffers": alloc_kind + " (payload, matrix); engine scratch (slots): "
+                       + ("sda_hbm_alloc chunks" if os.environ.get("SDA_SCRATCH_HBM") == "1" else "hipMalloc"),
             "decode_combine_matrix_ms": mx_ms,
             "decode_combine_fused_ms": cm_ms,
             "encode_ms": e_ms, "encode_hbm_GBps": (payload + 8.0 * Nc * Dc) / (e_ms * 1e-3) / 1e9,
@@ -775,7 +777,7 @@ def main():
             "ms": s_ms, "payload_GBps": total / (s_ms * 1e-3) / 1e9,
             "hbm_GBps": 2.0 * total / (s_ms * 1e-3) / 1e9,
             "roofline_frac": 2.0 * total / (s_ms * 1e-3) / 8.0e12,
-            "d2d_copy_ms": cp_ms, "d2d_copy_hbm_GBps": 2.0 * total / (cp_ms * 1e-3) / 1e9,
+            "d2d_copy_ms": cp_ms, "d2d_copy_hbm_GBps": 2.0 * total / (cp_ms * 1e-3) / 1e9, "buffers": alloc_kind,
             "note": "call time (host plan of one entry per blob + upload + kernel), HIP events",
         }
         log(f"[snapshot] {json.dumps(side['snapshot'])}")
@@ -835,6 +837,8 @@ def main():
             "participant_ms": p_ms, "participant_secrets_per_s": Dp / (p_ms * 1e-3),
             "participant_canonical_ms": pc_ms,
             "recipient_seeds": Ns, "recipient_ms": r_ms,
+            "buffers": "torch.empty (inputs, shares, payloads); engine scratch: "
+                       + ("sda_hbm_alloc chunks >= 256 MiB" if os.environ.get("SDA_SCRATCH_HBM") == "1" else "hipMalloc"),
             "recipient_mask_elems_per_s": Ns * Dp / (r_ms * 1e-3),
         }
         log(f"[pipelines] {json.dumps(side['pipelines'])}")

@@ -122,13 +122,44 @@ sda_status ok() {
         }                                                                                          \
     } while (0)
 
+// Engine scratch comes from hipMalloc.  SDA_SCRATCH_HBM=1 takes scratch of at least kScratchHbmMin bytes from
+// sda_hbm_alloc's chunk-mapped backing instead: on a clean box that measured 1.5 % slower for
+// the codec's 4 GB slot buffer and neutral for the pipelines (profiles/r05f/ab_scratch_hbm.txt), the same
+// direction as the combine's input (§4.1), so it stays opt-in for boxes whose VRAM is fragmented.
+constexpr size_t kScratchHbmMin = (size_t)256 << 20;
+bool scratch_hbm(size_t bytes) {
+    static const bool on = [] {
+        const char* e = getenv("SDA_SCRATCH_HBM");
+        return e && atoi(e) == 1;
+    }();
+    return on && bytes >= kScratchHbmMin;
+}
+bool hbm_owned(void* p);      // (HBM section) p was returned by sda_hbm_alloc and not freed
+
+void dev_free(void* p) {
+    if (!p) return;
+    if (hbm_owned(p)) (void)sda_hbm_free(p);     // pooled; reused only after a device sync (§2)
+    else (void)hipFree(p);
+}
+
+sda_status dev_alloc(void** p, size_t bytes) {
+    *p = nullptr;
+    if (scratch_hbm(bytes)) {
+        int d = 0;
+        HIP_TRY(hipGetDevice(&d));
+        return sda_hbm_alloc(d, bytes, p);
+    }
+    HIP_TRY(hipMalloc(p, bytes));
+    return SDA_OK;
+}
+
 sda_status ensure(void** buf, size_t* have, size_t need) {
     if (need <= *have) return SDA_OK;
-    if (*buf) (void)hipFree(*buf);
+    dev_free(*buf);
     *buf = nullptr;
     *have = 0;
     size_t want = need + need / 4 + 4096;
-    HIP_TRY(hipMalloc(buf, want));
+    if (sda_status e = dev_alloc(buf, want)) return e;
     *have = want;
     return SDA_OK;
 }
@@ -360,18 +391,18 @@ void sda_engine_destroy(sda_engine* h) {
     h->sub.clear();
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();            // _dev work may still be queued on callers' streams
-    if (h->work) (void)hipFree(h->work);
-    if (h->gen_log) (void)hipFree(h->gen_log);
-    if (h->codec_work) (void)hipFree(h->codec_work);
-    if (h->codec_mat) (void)hipFree(h->codec_mat);
-    if (h->pipe) (void)hipFree(h->pipe);
-    if (h->snap) (void)hipFree(h->snap);
-    if (h->stage) (void)hipFree(h->stage);
+    dev_free(h->work);
+    dev_free(h->gen_log);
+    dev_free(h->codec_work);
+    dev_free(h->codec_mat);
+    dev_free(h->pipe);
+    dev_free(h->snap);
+    dev_free(h->stage);
     sda::free_table(h->gen_tab);
     sda::free_table(h->rev_tab);
     if (h->rej_host) (void)hipHostFree(h->rej_host);
     if (h->hs_pin) (void)hipHostFree(h->hs_pin);
-    if (h->hs_dev) (void)hipFree(h->hs_dev);
+    dev_free(h->hs_dev);
     for (int b = 0; b < 2; ++b) {
         if (h->h2d_done[b]) (void)hipEventDestroy(h->h2d_done[b]);
         if (h->tile_free[b]) (void)hipEventDestroy(h->tile_free[b]);
@@ -386,7 +417,11 @@ void sda_engine_destroy(sda_engine* h) {
 sda_status sda_engine_synchronize(sda_engine* h) {
     SDA_ENTRY;
     if (!h) return fail(SDA_ERR_INVALID_ARGUMENT, "engine handle is NULL");
-    HIP_TRY(hipDeviceSynchronize());
+    for (size_t g = 0; g < (h->sub.empty() ? 1 : h->sub.size()); ++g) {   // every device of a multi-device handle
+        HIP_TRY(hipSetDevice(h->sub.empty() ? h->device : h->sub[g]->device));
+        HIP_TRY(hipDeviceSynchronize());
+    }
+    HIP_TRY(hipSetDevice(h->device));
     return ok();
 }
 
@@ -924,6 +959,11 @@ void hbm_release(void* ptr, HbmBuffer& b, size_t mapped_chunks) {
         (void)hipMemAddressFree(ptr, b.bytes);
     else if (b.device >= 0 && b.device < kHbmMaxDev)
         g_hbm_retired[b.device] += b.bytes;
+}
+
+bool hbm_owned(void* p) {
+    std::lock_guard<std::mutex> lk(g_hbm_mu);
+    return g_hbm.count(reinterpret_cast<uintptr_t>(p)) != 0;
 }
 
 uint64_t hbm_pooled_bytes(int device) {   // g_hbm_mu held
@@ -1830,10 +1870,10 @@ sda_status host_stream_ensure(sda_engine* h, size_t tile_bytes, size_t acc_bytes
     }
     const size_t dev_need = 2 * rup(tile_bytes) + rup(acc_bytes);
     if (h->hs_dev_bytes < dev_need) {
-        if (h->hs_dev) (void)hipFree(h->hs_dev);
+        dev_free(h->hs_dev);
         h->hs_dev = nullptr;
         h->hs_dev_bytes = 0;
-        HIP_TRY(hipMalloc(&h->hs_dev, dev_need));
+        if (sda_status e = dev_alloc(&h->hs_dev, dev_need)) return e;
         h->hs_dev_bytes = dev_need;
     }
     return SDA_OK;
