@@ -254,7 +254,8 @@ def host_path_leg(args, torch, eng, shares, N, D, m, dev, st):
     t = statistics.median(times)
     gbps = 8.0 * N * D / t / 1e9
     del host, hn, rows
-    return {"config": f"sda_share_combine (host entry point) over {N:,} host rows x {D:,} i64 (the headline job)",
+    return {"config": f"sda_share_combine (host entry point) over {N:,} host rows x {D:,} i64"
+                      + (" (the headline job)" if D == 1_000_000 else " (configs[3]'s resident tile)"),
             "ms_per_call": round(t * 1e3, 1), "GBps": round(gbps, 2), "calls": len(times),
             "h2d_pinned_GBps": round(pinned_gbps, 2), "h2d_pageable_GBps": round(pageable_gbps, 2),
             "frac_of_pinned_h2d": round(gbps / pinned_gbps, 4),
@@ -547,8 +548,17 @@ def main():
                 "passes": sst.passes,
                 "check": "bit-exact on 256 sampled columns: the reference recurrence over all ranks' rows in order"}
             log(f"[combine_signed_split] {json.dumps(side['combine_signed_split'])}")
-        if not args.no_host_path and world == 1 and not tile and args.only is None:
-            side["host_path"] = host_path_leg(args, torch, eng, shares, N, D, m, dev, stream())
+        if not args.no_host_path and world == 1 and args.only is None:
+            # configs[1]: the whole job from host rows.  configs[3]: the resident 1000-row tile from host rows
+            # (80 GB), and the PCIe-inclusive time of this GPU's whole share projected at that rate (SURVEY
+            # §8(d) C4: report kernel-only and end-to-end separately)
+            R = tile if tile else N
+            side["host_path"] = host_path_leg(args, torch, eng, shares, R, D, m, dev, stream())
+            if tile:
+                job = 8.0 * N * D
+                side["host_path"]["job_bytes_per_gpu"] = job
+                side["host_path"]["projected_job_s_host_path"] = round(job / (side["host_path"]["GBps"] * 1e9), 2)
+                side["host_path"]["job_s_hbm_resident"] = round(dt / args.steps, 3)
             log(f"[host_path] {json.dumps(side['host_path'])}")
         del shares
         torch.cuda.empty_cache()         # the next leg gets fresh allocations, not a reused segment
