@@ -721,6 +721,27 @@ def main():
             if not (torch.equal(torch.remainder(r, m), torch.remainder(x[:, cols].sum(0), m))
                     and bool((r.abs() < m).all())):
                 raise SystemExit("codec decode+combine FAILED")
+        # the clerk's HOST entry point over the same payloads (the Rust shim's call after the sealed-box opens):
+        # the payload bytes cross PCIe, the decode and combine run on device (engine.cpp host_decode_combine)
+        host_dc = None
+        if not args.no_host_path and world == 1:
+            from sda_amd import schemes as S_
+            hpay = buf[:int(payload) + 32].cpu().numpy()
+            hts = []
+            for i in range(3):
+                t0 = time.perf_counter()
+                hres = eng.clerk_decode_combine_packed(S_.Additive(3, m), hpay, off)
+                if i:
+                    hts.append(time.perf_counter() - t0)
+            torch.cuda.synchronize()
+            if not args.no_check and not np.array_equal(hres, cout.cpu().numpy()):
+                raise SystemExit("host decode+combine FAILED")
+            ht = statistics.median(hts)
+            host_dc = {"ms_per_call": round(ht * 1e3, 1), "payload_GBps": round(payload / ht / 1e9, 2),
+                       "shares_per_s": Nc * Dc / ht,
+                       "note": "sda_clerk_decode_combine from host memory: payload over PCIe (4.94 B/share instead "
+                               "of 8 for decoded rows), decoded + combined on device; equals the device path"}
+            del hpay
         e_ms, d_ms, c_ms = et.mean_ms(), dt_.mean_ms(), ct.mean_ms()
         mx_ms, cm_ms = alt["matrix"].mean_ms(), alt["fused"].mean_ms()
         default_path = os.environ.get("SDA_CODEC_PATH", "slots")
@@ -746,6 +767,7 @@ def main():
             "decode_combine_matrix_ms": mx_ms,
             "decode_combine_fused_ms": cm_ms,
             "encode_ms": e_ms, "encode_hbm_GBps": (payload + 8.0 * Nc * Dc) / (e_ms * 1e-3) / 1e9,
+            **({"host_decode_combine": host_dc} if host_dc else {}),
         }
         log(f"[codec] {json.dumps(side['codec'])}")
         del x, buf, mat

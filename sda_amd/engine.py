@@ -317,6 +317,22 @@ class Engine:
         _check(self.lib.sda_varint_decode(self.h, src, len(data), _ptr(out), out.size, C.byref(olen)))
         return out[: olen.value]
 
+    def clerk_decode_combine_packed(self, scheme, payload: np.ndarray, blob_off) -> np.ndarray:
+        """sda_clerk_decode_combine over blobs that sit back to back in one host uint8 array (blob i =
+        payload[blob_off[i]:blob_off[i + 1]]), passed as pointers into it: no per-blob copy on the Python side."""
+        s = scheme.c()
+        pay = np.ascontiguousarray(payload, dtype=np.uint8)
+        off = _arr(blob_off, np.uint64)
+        n = off.size - 1
+        base = pay.ctypes.data
+        ptrs = (_u8p * max(n, 1))(*[C.cast(base + int(o), _u8p) for o in off[:-1]])
+        lens = (C.c_uint64 * max(n, 1))(*[int(off[i + 1] - off[i]) for i in range(n)])
+        cap = int(max(np.diff(off).max(initial=0), 1))
+        out = np.zeros(cap, np.int64)
+        olen = C.c_uint64(0)
+        _check(self.lib.sda_clerk_decode_combine(self.h, C.byref(s), ptrs, lens, n, _ptr(out), out.size, C.byref(olen)))
+        return out[: olen.value]
+
     def clerk_decode_combine(self, scheme, blobs: Sequence[bytes]) -> np.ndarray:
         """clerk.rs:79-86 after the sealed-box opens: decode each participation, combine."""
         s = scheme.c()

@@ -140,3 +140,46 @@ def test_share_combine_host_rows_large(engine, oracle):
     assert_same(got, dev_out.cpu().numpy(), "host vs device")
     cols = np.random.default_rng(1).choice(D, 512, replace=False)
     assert_same(got[cols], oracle.combine(P, np.ascontiguousarray(host[:, cols])), "oracle sample")
+
+
+def test_clerk_decode_combine_streams_blob_groups(engine, oracle, monkeypatch):
+    """sda_clerk_decode_combine (clerk.rs:79-86 after the sealed-box opens) through the streaming path: a 1 MiB
+    stage puts the 120 payloads in ~60 groups; signed field shares, a few raw i64 participations (10-byte
+    varints) and a malformed one (a run of continuation bytes, decoded as sodium.rs:82-88 does) give the
+    oracle's decode + combine bit for bit; the errors keep the reference's order across groups."""
+    from sda_amd import SdaError
+    from sda_amd import engine as E
+    monkeypatch.setenv("SDA_HOST_STAGE_MB", "1")
+    rng = np.random.default_rng(5)
+    N, D = 120, 100_003
+    x = rng.integers(-(P - 1), P, size=(N, D), dtype=np.int64)
+    x[17] = rng.integers(-(1 << 62), 1 << 62, size=D, dtype=np.int64)
+    x[90, :5] = [np.iinfo(np.int64).min, np.iinfo(np.int64).max, -1, 0, 1 << 40]
+    blobs = [oracle.varint_encode(r) for r in x]
+    mal = bytearray(blobs[64])
+    mal[1000:1000 + 12] = b"\x80" * 12                       # one 11+-byte run: sodium.rs decodes it anyway
+    blobs[64] = bytes(mal)
+    rows = [oracle.varint_decode(b) for b in blobs]
+    same_len = all(r.size == D for r in rows)
+    got = None
+    if same_len:
+        got = engine.clerk_decode_combine(S.Additive(3, P), blobs)
+        assert_same(got, oracle.combine(P, np.stack(rows)), "streamed decode+combine")
+    else:                                                    # the malformed run changed the length: Wrong dimension
+        with pytest.raises(SdaError) as ei:
+            engine.clerk_decode_combine(S.Additive(3, P), blobs)
+        assert ei.value.status == E.ERR_WRONG_DIMENSION and "participation 64" in str(ei.value)
+        blobs[64] = oracle.varint_encode(x[64])
+        got = engine.clerk_decode_combine(S.Additive(3, P), blobs)
+        assert_same(got, oracle.combine(P, x), "streamed decode+combine")
+    # a participation in a late group of another length: Err("Wrong dimension") naming it
+    bad = list(blobs)
+    bad[101] = oracle.varint_encode(x[101][:-1])
+    with pytest.raises(SdaError) as ei:
+        engine.clerk_decode_combine(S.Additive(3, P), bad)
+    assert ei.value.status == E.ERR_WRONG_DIMENSION and "participation 101" in str(ei.value)
+    # m = 0: participation 0 is folded before any other length is checked (combiner.rs:20-25)
+    with pytest.raises(SdaError) as ei:
+        engine.clerk_decode_combine(S.Additive(3, 0), bad)
+    assert ei.value.status == E.ERR_PRECONDITION
+    assert engine.clerk_decode_combine(S.Additive(3, 0), [b"", b""]).size == 0
