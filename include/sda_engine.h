@@ -323,7 +323,8 @@ sda_status sda_recipient_reveal_dev(sda_engine* h, const sda_masking_scheme* ms,
                                     int32_t mode, int64_t* out, uint64_t out_cap, uint64_t* out_len,
                                     void* stream);
 /* Host form: mask rows as MaskCombiner::combine takes them (Full masks / ChaCha seeds-as-i64),
- * share rows as SecretReconstructor::reconstruct takes them. */
+ * share rows as SecretReconstructor::reconstruct takes them.  On a multi-device handle the ChaCha mask
+ * combine is split over the devices (as sda_mask_combine), the rest runs on ordinals[0]. */
 sda_status sda_recipient_reveal(sda_engine* h, const sda_masking_scheme* ms,
                                 const int64_t* const* mask_rows, const uint64_t* mask_lens, uint64_t n_masks,
                                 const sda_sharing_scheme* ss, uint64_t dimension, const uint64_t* indices,

@@ -320,6 +320,9 @@ sda_status host_combine(sda_engine* h, int64_t m, const int64_t* const* rows, ui
 sda_status host_chacha_combine(sda_engine* h, int64_t m, uint64_t D, const std::vector<uint32_t>& seeds, uint32_t w,
                                uint64_t n, int64_t* out_host);
 void destroy_comms(sda_engine* h);
+sda_status chacha_combine_multi(sda_engine* h, int64_t m, uint64_t D, const std::vector<uint32_t>& seeds, uint32_t w,
+                                uint64_t n, int64_t* dst);
+sda_status host_stream_ensure(sda_engine* h, size_t tile_bytes, size_t acc_bytes);
 sda_status host_decode_combine(sda_engine* h, int64_t m, const uint8_t* const* blobs, const uint64_t* lens, uint64_t n,
                                int64_t* out, uint64_t out_cap, uint64_t* out_len);
 sda_status host_additive_generate(sda_engine* h, int64_t m, uint64_t n, const int64_t* secrets, uint64_t D,
@@ -1644,6 +1647,19 @@ sda_status sda_recipient_reveal(sda_engine* h, const sda_masking_scheme* ms, con
             if (mask_lens[i]) return fail(SDA_ERR_PRECONDITION, "assertion failed: masks.iter().all(|mask| mask.len() == 0)");
     }
     const uint64_t outn = ss->kind == SDA_SHARING_ADDITIVE ? share_len : dimension;
+    // A multi-device handle spreads the mask combine (receive.rs:113-116, the dominant cost at configs[4]) over its
+    // devices -- seeds split, one RCCL reduce onto device 0 (host path section) -- and runs the rest of the
+    // pipeline on device 0 with the combined mask as one Full mask row: (0 + c) % m = c for the canonical c, so
+    // the unmask sees the same mask.  Only where the reference would not panic in the mask combine (m > 0).
+    const sda_masking_scheme full_row = {SDA_MASKING_FULL, ms->modulus, 0, 0};
+    const bool multi_mask = ms->kind == SDA_MASKING_CHACHA && !h->sub.empty() && n_masks && ms->dimension &&
+                            ms->modulus > 0;
+    if (multi_mask) {
+        if (sda_status e = host_stream_ensure(h, 0, ms->dimension * 8)) return e;
+        if (sda_status e = chacha_combine_multi(h, ms->modulus, ms->dimension, seeds, (uint32_t)width, n_masks,
+                                                static_cast<int64_t*>(h->hs_dev)))
+            return e;
+    }
     DevArena a;
     if (sda_status e = stage(h, rup(n_idx * share_len * 8 + 8) + rup(n_masks * width * 8 + 8) + rup(outn * 8 + 8), &a))
         return e;
@@ -1656,12 +1672,15 @@ sda_status sda_recipient_reveal(sda_engine* h, const sda_masking_scheme* ms, con
         for (uint64_t i = 0; i < n_masks; ++i)
             if (width) HIP_TRY(hipMemcpyAsync(static_cast<int64_t*>(dmask) + i * width, mask_rows[i], width * 8,
                                               hipMemcpyHostToDevice, h->stream));
-    if (ms->kind == SDA_MASKING_CHACHA && !seeds.empty())
+    if (ms->kind == SDA_MASKING_CHACHA && !seeds.empty() && !multi_mask)
         HIP_TRY(hipMemcpyAsync(dmask, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, h->stream));
     uint64_t len = 0;
-    if (sda_status e = recipient_pipeline(h, ms, dmask, n_masks, ms->kind == SDA_MASKING_NONE ? 0 : width, ss,
-                                          dimension, indices, dsh, n_idx, share_len, output_modulus, mode, dout,
-                                          (uint64_t)-1, &len, h->stream))
+    if (sda_status e = multi_mask
+                           ? recipient_pipeline(h, &full_row, h->hs_dev, 1, ms->dimension, ss, dimension, indices, dsh,
+                                                n_idx, share_len, output_modulus, mode, dout, (uint64_t)-1, &len, h->stream)
+                           : recipient_pipeline(h, ms, dmask, n_masks, ms->kind == SDA_MASKING_NONE ? 0 : width, ss,
+                                                dimension, indices, dsh, n_idx, share_len, output_modulus, mode, dout,
+                                                (uint64_t)-1, &len, h->stream))
         return e;
     if (out_cap < len) return fail(SDA_ERR_INVALID_ARGUMENT, "output buffer too small");
     if (len) HIP_TRY(hipMemcpyAsync(out, dout, len * 8, hipMemcpyDeviceToHost, h->stream));
@@ -2033,10 +2052,11 @@ void destroy_comms(sda_engine* h) {
     h->comms = nullptr;
 }
 
-// chacha.rs:57-76 over host seed words [n][w] (combined into out_host, D values): seeds split over the devices,
-// one RCCL reduce onto device 0 (section comment)
-sda_status host_chacha_combine(sda_engine* h, int64_t m, uint64_t D, const std::vector<uint32_t>& seeds, uint32_t w,
-                               uint64_t n, int64_t* out_host) {
+// chacha.rs:57-76 over host seed words [n][w], the combined mask (D values) left in dst on device 0 (ordered on
+// h->stream; the other devices are idle again at return): seeds split over the devices, one RCCL reduce onto
+// device 0 (section comment).  dst must not lie in device 0's staging arena or work buffer.
+sda_status chacha_combine_multi(sda_engine* h, int64_t m, uint64_t D, const std::vector<uint32_t>& seeds, uint32_t w,
+                                uint64_t n, int64_t* dst) {
     // (a one-device handle from sda_engine_create_multi takes the split path too: a one-rank reduce)
     const size_t G = n_devices(h);
     const bool split = !h->sub.empty() && distinct_devices(h) && n >= G && !sda::chacha_needs_stream_path(m) &&
@@ -2050,35 +2070,43 @@ sda_status host_chacha_combine(sda_engine* h, int64_t m, uint64_t D, const std::
         uint64_t s0 = 0, cnt = n;
         if (split) shard(n, g, G, &s0, &cnt);
         DevArena a;
-        if (sda_status e = stage(d, rup(cnt * w * 4 + 4) + 2 * rup(D * 8), &a)) return e;
+        if (sda_status e = stage(d, rup(cnt * w * 4 + 4) + rup(D * 8), &a)) return e;
         uint32_t* dseeds = a.take<uint32_t>(cnt * w + 1);
-        partial[g] = a.take<int64_t>(D);
+        partial[g] = split ? a.take<int64_t>(D) : dst;
         if (cnt) HIP_TRY(hipMemcpyAsync(dseeds, seeds.data() + s0 * w, cnt * w * 4, hipMemcpyHostToDevice, d->stream));
         return chacha_combine(d, m, D, dseeds, w, cnt, partial[g], d->stream);
     });
     if (st) return st;
-    int64_t* res = partial[0];
-    if (split) {
-        if (sda_status e = ensure_comms(h)) return e;
-        Rccl& r = rccl();
-        NCCL_TRY(r.group_start());
-        for (size_t g = 0; g < G; ++g) {
-            sda_engine* d = dev_of(h, g);
-            ncclResult_t rr = r.reduce(partial[g], partial[g], D, ncclInt64, ncclSum, 0,
-                                       static_cast<ncclComm_t>(h->comms[g]), d->stream);
-            if (rr != ncclSuccess) {
-                (void)r.group_end();
-                return fail(SDA_ERR_DEVICE, "ncclReduce: %s", r.error_string(rr));
-            }
-        }
-        NCCL_TRY(r.group_end());
-        HIP_TRY(hipSetDevice(h->device));
-        res = partial[0] + rup(D * 8) / 8;                     // the arena's second D-slot on device 0
-        HIP_TRY(sda::launch_mod_canonical(partial[0], D, res, m, h->stream));
-    }
     HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(hipMemcpyAsync(out_host, res, D * 8, hipMemcpyDeviceToHost, h->stream));
-    for (size_t g = 0; g < parts; ++g) HIP_TRY(hipStreamSynchronize(dev_of(h, g)->stream));
+    if (!split) return SDA_OK;
+    if (sda_status e = ensure_comms(h)) return e;
+    Rccl& r = rccl();
+    NCCL_TRY(r.group_start());
+    for (size_t g = 0; g < G; ++g) {
+        sda_engine* d = dev_of(h, g);
+        ncclResult_t rr = r.reduce(partial[g], partial[g], D, ncclInt64, ncclSum, 0,
+                                   static_cast<ncclComm_t>(h->comms[g]), d->stream);
+        if (rr != ncclSuccess) {
+            (void)r.group_end();
+            return fail(SDA_ERR_DEVICE, "ncclReduce: %s", r.error_string(rr));
+        }
+    }
+    NCCL_TRY(r.group_end());
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(sda::launch_mod_canonical(partial[0], D, dst, m, h->stream));
+    for (size_t g = 1; g < G; ++g) HIP_TRY(hipStreamSynchronize(dev_of(h, g)->stream));   // reduce sent
+    return SDA_OK;
+}
+
+// the same, the combined mask copied to out_host (MaskCombiner::combine)
+sda_status host_chacha_combine(sda_engine* h, int64_t m, uint64_t D, const std::vector<uint32_t>& seeds, uint32_t w,
+                               uint64_t n, int64_t* out_host) {
+    HIP_TRY(hipSetDevice(h->device));
+    if (sda_status e = host_stream_ensure(h, 0, D * 8)) return e;          // dst: the host path's accumulator
+    int64_t* dst = static_cast<int64_t*>(h->hs_dev);
+    if (sda_status e = chacha_combine_multi(h, m, D, seeds, w, n, dst)) return e;
+    HIP_TRY(hipMemcpyAsync(out_host, dst, D * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
     return SDA_OK;
 }
 

@@ -183,3 +183,27 @@ def test_clerk_decode_combine_streams_blob_groups(engine, oracle, monkeypatch):
         engine.clerk_decode_combine(S.Additive(3, 0), bad)
     assert ei.value.status == E.ERR_PRECONDITION
     assert engine.clerk_decode_combine(S.Additive(3, 0), [b"", b""]).size == 0
+
+
+@pytest.mark.parametrize("handle", ["multi1", "multi3"])
+def test_recipient_reveal_multi_handle(request, handle):
+    """sda_recipient_reveal (receive.rs:80-157 + positive()) on a multi-device handle: the ChaCha mask combine runs
+    through the seed split (one-rank RCCL reduce on multi1, one device on the repeated-ordinal multi3), the rest on
+    device 0 with the combined mask as a Full row; equal to the step-wise oracle flow for every ChaCha case of
+    test_gpu_pipelines (the full_loop KAT included), both clerk orders."""
+    from tests.oracle_backend import OracleBackend
+    from tests.pipeline import Draws, run_aggregation
+    from tests.test_gpu_pipelines import _cases
+    eng = request.getfixturevalue(handle)
+    for name, ms, ss, m, D, inputs, expected in _cases():
+        if not isinstance(ms, S.ChaChaMasking):
+            continue
+        tr = run_aggregation(OracleBackend(), ms, ss, m, D, inputs, Draws(0x5DA))
+        n = ss.output_size()
+        for order in (list(range(n)), list(reversed(range(n)))):
+            if isinstance(ss, S.PackedShamir):
+                order = order[: ss.reconstruction_threshold() + 1]
+            indexed = [(c, tr.clerk_results[c]) for c in order]
+            be = OracleBackend()
+            exp = be.positive(m, be.secret_unmask(ms, (be.mask_combine(ms, tr.masks), be.secret_reconstruct(ss, D, indexed))))
+            assert_same(eng.recipient_reveal(ms, tr.masks, ss, D, indexed, m), exp, f"{handle} {name}")
