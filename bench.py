@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the host-path leg (sda_share_combine from host rows at the headline size)")
     ap.add_argument("--host-calls", type=int, default=2, help="timed sda_share_combine calls in the host-path leg")
+    ap.add_argument("--no-multi-device", action="store_true",
+                    help="skip the in-process multi-GPU leg (one engine handle over every visible GPU, N = 1 only)")
+    ap.add_argument("--multi-device-leg", default=None, help=argparse.SUPPRESS)   # internal: the child's ordinals
     ap.add_argument("--no-signed-split", action="store_true",
                     help="N > 1: skip the signed-shares leg of the participation split (two-pass path)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -208,6 +211,98 @@ def cpu_baseline_chacha(threads: int, budget_s: float):
                       "runs; oracle/sda_oracle.c at -O2"}
 
 
+def multi_device_leg(args):
+    """The drop-in boundary over every GPU of the node from ONE process (sda_engine_create_multi):
+    runs in a child process (started before this one touches a GPU; killed after 300 s) and returns its record,
+    or None with one visible GPU.  SDA_BENCH_MULTI_DEVICES="0,0" rehearses it on one GPU (slices on one device)."""
+    import subprocess
+    forced = os.environ.get("SDA_BENCH_MULTI_DEVICES")
+    if forced:
+        devs = forced
+    else:
+        import torch
+        n = torch.cuda.device_count()          # counts devices without initialising them
+        if n < 2:
+            return None
+        devs = ",".join(str(i) for i in range(n))
+    cmd = [sys.executable, os.path.abspath(__file__), "--multi-device-leg", devs, "--rows", str(args.rows),
+           "--dim", str(args.dim)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 300 s", "devices": devs}
+    sys.stderr.write(r.stderr[-4000:])
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"exit {r.returncode}: {r.stderr.strip().splitlines()[-1] if r.stderr.strip() else ''}",
+                "devices": devs}
+    return json.loads(lines[-1])
+
+
+def multi_device_child(args):
+    """multi_device_leg's process: one engine handle over the given ordinals.
+    (1) ShareCombiner::combine (clerk.rs:85-86) over the headline job's N x D i64 rows in host memory: the
+        handle streams a column slice per GPU; timed against a one-GPU handle on the same rows, bit-exact.
+    (2) MaskCombiner::combine (chacha.rs:57-76) of 2048 ChaCha seeds over a 10M-dim mask: seeds split over the
+        GPUs and one RCCL ncclReduce (int64) over xGMI; bit-exact against the one-GPU handle."""
+    import torch
+    from sda_amd import Engine, schemes as S
+    devs = [int(x) for x in args.multi_device_leg.split(",")]
+    N, D, m = args.rows, args.dim, MODULUS
+    one = Engine(devs[0])
+    eng = Engine(devices=devs)
+    dev = torch.device("cuda", devs[0])
+    host = torch.empty((N, D), dtype=torch.int64)
+    tile = max(1, min(N, (8 << 30) // (8 * D)))
+    t = torch.empty((tile, D), dtype=torch.int64, device=dev)
+    for r0 in range(0, N, tile):
+        r = min(tile, N - r0)
+        one.synth_fill_dev(t.data_ptr(), r, D, SEED_BASE + 1 + r0, -(m - 1), m, torch.cuda.current_stream().cuda_stream)
+        host[r0:r0 + r].copy_(t[:r])
+    del t
+    torch.cuda.synchronize()
+    hn = host.numpy()
+    rows = [hn[i] for i in range(N)]
+    sch = S.Additive(3, m)
+
+    def timed(e, calls=2):
+        ts, res = [], None
+        for i in range(1 + calls):
+            t0 = time.perf_counter()
+            res = e.share_combine(sch, rows)
+            if i:
+                ts.append(time.perf_counter() - t0)
+        return statistics.median(ts), res
+    t1, r1 = timed(one)
+    tg, rg = timed(eng)
+    ok = bool(np.array_equal(r1, rg))
+    Dc, Ns = 10_000_000, 2048
+    seeds = [list(map(int, row)) for row in np.random.default_rng(SEED_BASE + 5).integers(0, 1 << 32, size=(Ns, 4))]
+    ms = S.ChaChaMasking(m, Dc, 128)
+    def timed_mask(e, calls=3):                    # one warm call, then the median of `calls`
+        ts, res = [], e.mask_combine(ms, seeds)
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            res = e.mask_combine(ms, seeds)
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts), res
+    tc1, c1 = timed_mask(one)
+    tcg, cg = timed_mask(eng)
+    okc = bool(np.array_equal(c1, cg))
+    rec = {"devices": devs, "device_count": eng.device_count(),
+           "share_combine": {"config": f"{N:,} host rows x {D:,} i64, signed (the headline job from host memory)",
+                             "one_gpu_s": round(t1, 3), "one_gpu_GBps": round(8.0 * N * D / t1 / 1e9, 2),
+                             "all_gpus_s": round(tg, 3), "all_gpus_GBps": round(8.0 * N * D / tg / 1e9, 2),
+                             "split": "columns", "bit_exact_vs_one_gpu": ok},
+           "chacha_mask_combine": {"config": f"{Ns} seeds x {Dc:,}-dim (host call)",
+                                   "one_gpu_s": round(tc1, 4), "all_gpus_s": round(tcg, 4),
+                                   "all_gpus_mask_elems_per_s": Ns * Dc / tcg,
+                                   "split": "seeds + RCCL ncclReduce int64 onto ordinals[0]", "bit_exact_vs_one_gpu": okc}}
+    print(json.dumps(rec), flush=True)
+    if not (ok and okc):
+        sys.exit(3)
+
+
 def host_path_leg(args, torch, eng, shares, N, D, m, dev, st):
     """The drop-in boundary at the headline size: ShareCombiner::combine (clerk.rs:85-86 -> combiner.rs:16-28)
     through the HOST entry point the Rust shim calls, sda_share_combine, over the same N x D i64 rows held in
@@ -350,8 +445,15 @@ def spawn_ranks(n: int) -> int:
 
 def main():
     args = parse()
+    if args.multi_device_leg is not None:
+        multi_device_child(args)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
+    multi = None
+    if (os.environ.get("WORLD_SIZE", "1") == "1" and args.only is None and args.config == 1 and not args.no_multi_device
+            and not args.no_host_path):
+        multi = multi_device_leg(args)         # before this process touches a GPU (a child process of its own)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -914,6 +1016,8 @@ def main():
         if dist_info is not None:
             rec["dist"] = dist_info
         rec.update(side)
+        if multi is not None:
+            rec["multi_device"] = multi
         if world == 1 and not args.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(min(D, 1_000_000), args.cpu_seconds)
         print(json.dumps(rec), flush=True)

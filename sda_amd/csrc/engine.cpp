@@ -1822,12 +1822,13 @@ long long env_ll(const char* name, long long dflt) {
     return e && *e ? atoll(e) : dflt;
 }
 
-// host threads for packing rows into pinned memory (SDA_HOST_THREADS; default: the CPUs, at most 16)
-int host_threads() {
+// host threads for packing rows into pinned memory, over all the handle's devices (SDA_HOST_THREADS; default:
+// the CPUs, at most 16 per device)
+int host_threads(size_t devices = 1) {
     const long long t = env_ll("SDA_HOST_THREADS", 0);
-    if (t > 0) return (int)std::min<long long>(t, 256);
+    if (t > 0) return (int)std::min<long long>(t, 1024);
     const unsigned hc = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(hc ? hc : 1u, 16u));
+    return (int)std::max<unsigned>(1u, std::min<unsigned>(hc ? hc : 1u, 16u * (unsigned)devices));
 }
 
 // bytes of one staging tile (SDA_HOST_STAGE_MB, default 256 MiB; at least 1 MiB)
@@ -1972,7 +1973,7 @@ sda_engine* dev_of(sda_engine* h, size_t g) { return h->sub.empty() ? h : h->sub
 sda_status host_combine(sda_engine* h, int64_t m, const int64_t* const* rows, uint64_t n_rows, uint64_t dim,
                         int64_t* out) {
     const size_t G = n_devices(h);
-    const int T = std::max(1, host_threads() / (int)G);
+    const int T = std::max(1, host_threads(G) / (int)G);
     return for_devices(h, [&](size_t g) -> sda_status {
         uint64_t lo, w;
         column_slice(dim, g, G, &lo, &w);
