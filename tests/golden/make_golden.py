@@ -8,6 +8,11 @@ Pinning:
     this script asserts them before writing.
   * chacha_rfc7539.json holds the RFC 7539 block-function vectors (section 2.3.2 and A.1 #1),
     typed in from the RFC, not produced by the oracle; the oracle is asserted against them.
+  * rand03_chacharng.json holds the known answers of rand 0.3's own ChaChaRng test (`test_rng_true_values`
+    in the crate's src/chacha.rs: 32 words of the zero key, then the i-th word of the i-th block for the
+    seed [0, 1, .., 7]), typed in from that test (the crate is absent from the image); the oracle is
+    asserted against them.  They pin ChaChaRng::from_seed's key layout, the block counter and next_u32's
+    order, i.e. the stream chacha.rs:36/67 draws from.
   * every other value is the oracle's restatement output (a regression pin for the GPU path).
 """
 from __future__ import annotations
@@ -71,6 +76,20 @@ def trace_json(tr):
             "masked_output": L(tr.masked_output), "output": L(tr.output), "positive": L(tr.positive)}
 
 
+# rand 0.3, src/chacha.rs, test_rng_true_values: ChaChaRng::from_seed(&[0u32; 8]), 32 x next_u32 (RFC 7539
+# test vectors 1 and 2: blocks 0 and 1 of the zero key) ...
+RAND03_ZERO_KEY = [
+    0xade0b876, 0x903df1a0, 0xe56a5d40, 0x28bd8653, 0xb819d2bd, 0x1aed8da0, 0xccef36a8, 0xc70d778b,
+    0x7c5941da, 0x8d485751, 0x3fe02477, 0x374ad8b8, 0xf4b8436a, 0x1ca11815, 0x69b687c3, 0x8665eeb2,
+    0xbee7079f, 0x7a385155, 0x7c97ba98, 0x0d082d73, 0xa0290fcb, 0x6965e348, 0x3e53c612, 0xed7aee32,
+    0x7621b729, 0x434ee69c, 0xb03371d5, 0xd539d874, 0x281fed31, 0x45fb0a51, 0x1f0ae1ac, 0x6f4d794b]
+# ... and from_seed(&[0, 1, 2, 3, 4, 5, 6, 7]): "the 17*i-th 32-bit word, i.e., the i-th word of the i-th
+# 16-word block" for i = 0..15
+RAND03_SEED_0_7_STRIDE17 = [
+    0xf225c81a, 0x6ab1be57, 0x04d42951, 0x70858036, 0x49884684, 0x64efec72, 0x4be2d186, 0x3615b384,
+    0x11cfa18e, 0xd3c50049, 0x75c775f6, 0x434c6530, 0x2c5bad8f, 0x898881dc, 0x5f1c86d9, 0xc1f8e7f4]
+
+
 def main():
     be = OracleBackend()
     out = {}
@@ -105,6 +124,22 @@ def main():
         streams.append({"seed": seed_words, "modulus": m, "first_u32": u32,
                         "gen_range": [r.gen_range(0, m) for _ in range(n)]})
     out["chacha_rfc7539.json"] = {"rfc7539": RFC7539, "rand03_streams": streams}
+
+    # 3b. rand 0.3 ChaChaRng's own known answers (external pin, typed in; see the module doc)
+    r = O.Rng([0] * 8)
+    got = [r.next_u32() for _ in range(32)]
+    assert got == RAND03_ZERO_KEY, [hex(x) for x in got]
+    r = O.Rng(list(range(8)))
+    got = []
+    for _ in range(16):
+        got.append(r.next_u32())
+        for _ in range(16):
+            r.next_u32()
+    assert got == RAND03_SEED_0_7_STRIDE17, [hex(x) for x in got]
+    out["rand03_chacharng.json"] = {
+        "source": "rand 0.3 src/chacha.rs test_rng_true_values (crate absent from the image; typed in)",
+        "zero_key_first_32_u32": RAND03_ZERO_KEY,
+        "seed_0_to_7_word_17i": RAND03_SEED_0_7_STRIDE17}
 
     # 4. combine order / overflow cases (combiner.rs:16-28)
     cases = [

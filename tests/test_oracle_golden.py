@@ -66,6 +66,22 @@ def test_rand03_streams(oracle):
         assert [r.gen_range(0, st["modulus"]) for _ in st["gen_range"]] == st["gen_range"]
 
 
+def test_rand03_chacharng_known_answers(oracle):
+    """rand 0.3's own ChaChaRng test (src/chacha.rs test_rng_true_values): the zero key's first 32 words and,
+    for the seed [0, 1, .., 7], the i-th word of the i-th block -- ChaChaRng::from_seed's key layout, its block
+    counter and next_u32's order, the stream chacha.rs:36/67 draws from."""
+    v = load("rand03_chacharng.json")
+    r = oracle.Rng([0] * 8)
+    assert [r.next_u32() for _ in range(32)] == v["zero_key_first_32_u32"]
+    r = oracle.Rng(list(range(8)))
+    got = []
+    for _ in range(16):
+        got.append(r.next_u32())
+        for _ in range(16):
+            r.next_u32()
+    assert got == v["seed_0_to_7_word_17i"]
+
+
 def test_stream_layout(oracle):
     """next_u64 = (next_u32 << 32) | next_u32; block counter starts at 0 (ChaCha20 zero key = RFC A.1#1)."""
     r = oracle.Rng([0, 0, 0, 0])
