@@ -121,6 +121,29 @@ constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
 #ifndef SDA_GEN_WAVES
 #define SDA_GEN_WAVES 4
 #endif
+// Wave priorities by phase (s_setprio) in the exact kernel: SDA_GEN_PRIO_LOAD while a wave issues its tile
+// loads, 0 during the transform, SDA_GEN_PRIO_STORE for its share stores -- so the memory phases of a CU's
+// waves are not starved by the other waves' VALU streams.  Exact share-gen 7.18-7.20 -> 7.01-7.02 ms and
+// 7.36 -> 7.19-7.21 ms on two boxes (3 interleaved rounds each, profiles/r05o, r05p); the canonical kernel,
+// memory-bound, got 1.5 % slower with it and runs without; so did the exact reveal.  SDA_GEN_PRIO = 0 turns it
+// off (A/B knob).
+#ifndef SDA_GEN_PRIO
+#define SDA_GEN_PRIO 1
+#endif
+#ifndef SDA_GEN_PRIO_AFTER_LDS
+#define SDA_GEN_PRIO_AFTER_LDS 0          // A/B knob: drop to 0 after the LDS reads instead of at the barrier
+#endif
+#ifndef SDA_GEN_PRIO_LOAD
+#define SDA_GEN_PRIO_LOAD 3
+#endif
+#ifndef SDA_GEN_PRIO_STORE
+#define SDA_GEN_PRIO_STORE 2
+#endif
+template <int LEVEL>
+__device__ __forceinline__ void set_prio() {
+    if constexpr (SDA_GEN_PRIO) __builtin_amdgcn_s_setprio(LEVEL);
+}
+
 // Waves per EU: 5 where the transform fits 102 VGPRs without spilling (canonical and lazy-exact at
 // L <= 16), else SDA_GEN_WAVES (4: 128 VGPRs).
 template <int L, bool CANON, bool LAZY>
@@ -213,6 +236,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
     constexpr int NR = N3 - 1;         // share rows (clerks); N3 = 3^ND so NR is even
     using Z = Zero3<L, N3>;
     const uint32_t tid = threadIdx.x;
+    if constexpr (!CANON) set_prio<SDA_GEN_PRIO_LOAD>();
     const uint32_t lane = tid & 63, half = lane >> 5;
     const uint32_t lb = (tid & ~63u) + 2 * (lane & 31) + half;       // this lane's batch in the tile
     const uint32_t pb_off = (tid & ~63u) + 2 * (lane & 31);          // first batch of its store pair
@@ -289,6 +313,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
             }
         }
         __syncthreads();
+        if constexpr (!CANON && !SDA_GEN_PRIO_AFTER_LDS) set_prio<0>();
 
         // values = [0, secrets, randomness]; lanes past B run on zeros and store nothing
         const uint64_t b = b0 + lb;
@@ -301,6 +326,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
             // (lanes past B read whatever the LDS holds: they log nothing, store nothing and count as in range)
             static_for<1, L>([&](auto i) { raw[i] = lds[lpos(((uint32_t)i <= k ? es : ed) + i)]; });
         }
+        if constexpr (!CANON && SDA_GEN_PRIO_AFTER_LDS) set_prio<0>();
         bool in_range = true;
         static_for<1, L>([&](auto i) { in_range = in_range && ((uint64_t)(raw[i] + (P - 1)) < (uint64_t)(2 * P - 1)); });
         // a dead lane's stale LDS words must not send its live partner to the fix-up kernel: it counts as in
@@ -479,6 +505,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         }
 
         // ---- shares = points[1..=n], clerk-major (batched.rs:46-48) ----
+        if constexpr (!CANON) set_prio<SDA_GEN_PRIO_STORE>();
         const uint64_t pb = b0 + pb_off;
         const bool st1 = pair_ok && pb + 1 < B;
         int64_t* orow = out + ((uint64_t)vec * NR + half) * B + pb;
