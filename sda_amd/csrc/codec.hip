@@ -310,10 +310,6 @@ __device__ __forceinline__ int64_t varint_value_at(const uint32_t* lb, uint32_t 
 // out + r * kSlotCap, and the region's element count to region_count[r]; region_base and blob_irregular
 // are not read.  A region with more than kSlotCap elements sets *wide, and so does a malformed blob (a run
 // of >= 11 continuation bytes always holds an element longer than 5 bytes).
-// SDA_CODEC_PRIO (A/B knob): the decode's region loads at wave priority 3 (s_setprio), the decode at 0.
-#ifndef SDA_CODEC_PRIO
-#define SDA_CODEC_PRIO 0
-#endif
 template <typename OutT, bool SPARSE = false>
 __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* __restrict__ bytes,
                                                                  const uint64_t* __restrict__ blob_region,
@@ -343,7 +339,6 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
     const bool interior = word * 16 >= begin + 16 && end > word * 16 + kRegionBytes;
     const uint4* p = reinterpret_cast<const uint4*>(bytes);
     uint4 v[kWPT];
-    if constexpr (SDA_CODEC_PRIO) __builtin_amdgcn_s_setprio(3);     // the region's loads issue first
 #pragma unroll
     for (int k = 0; k < kWPT; ++k) {
         const uint64_t wk = word + threadIdx.x + k * kThreads;
@@ -351,7 +346,6 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
     }
     uint4 h = make_uint4(0, 0, 0, 0);                         // the word before the region (thread 0)
     if (threadIdx.x == 0 && word * 16 > begin) h = p[word - 1];
-    if constexpr (SDA_CODEC_PRIO) __builtin_amdgcn_s_setprio(0);
     if (threadIdx.x == kThreads - 1) lb4[kThreads + 1] = make_uint4(0, 0, 0, 0);
     OutT* dst = SPARSE ? out + r * kSlotCap : out + (uint64_t)b * out_stride + region_base[r];
     bool narrow_fail = false;

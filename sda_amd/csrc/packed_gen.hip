@@ -124,14 +124,12 @@ constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
 // Wave priorities by phase (s_setprio) in the exact kernel: SDA_GEN_PRIO_LOAD while a wave issues its tile
 // loads, 0 during the transform, SDA_GEN_PRIO_STORE for its share stores -- so the memory phases of a CU's
 // waves are not starved by the other waves' VALU streams.  Exact share-gen 7.18-7.20 -> 7.01-7.02 ms and
-// 7.36 -> 7.19-7.21 ms on two boxes (3 interleaved rounds each, profiles/r05o, r05p); the canonical kernel,
+// 7.36 -> 7.19-7.21 ms and 7.14-7.16 -> 6.97-7.08 ms on three boxes (3 interleaved rounds each, profiles/r05o,
+// r05p, r05q; dropping to 0 after the LDS reads, or levels 2/1, measured the same); the canonical kernel,
 // memory-bound, got 1.5 % slower with it and runs without; so did the exact reveal.  SDA_GEN_PRIO = 0 turns it
 // off (A/B knob).
 #ifndef SDA_GEN_PRIO
 #define SDA_GEN_PRIO 1
-#endif
-#ifndef SDA_GEN_PRIO_AFTER_LDS
-#define SDA_GEN_PRIO_AFTER_LDS 0          // A/B knob: drop to 0 after the LDS reads instead of at the barrier
 #endif
 #ifndef SDA_GEN_PRIO_LOAD
 #define SDA_GEN_PRIO_LOAD 3
@@ -313,7 +311,7 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
             }
         }
         __syncthreads();
-        if constexpr (!CANON && !SDA_GEN_PRIO_AFTER_LDS) set_prio<0>();
+        if constexpr (!CANON) set_prio<0>();
 
         // values = [0, secrets, randomness]; lanes past B run on zeros and store nothing
         const uint64_t b = b0 + lb;
@@ -326,7 +324,6 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
             // (lanes past B read whatever the LDS holds: they log nothing, store nothing and count as in range)
             static_for<1, L>([&](auto i) { raw[i] = lds[lpos(((uint32_t)i <= k ? es : ed) + i)]; });
         }
-        if constexpr (!CANON && SDA_GEN_PRIO_AFTER_LDS) set_prio<0>();
         bool in_range = true;
         static_for<1, L>([&](auto i) { in_range = in_range && ((uint64_t)(raw[i] + (P - 1)) < (uint64_t)(2 * P - 1)); });
         // a dead lane's stale LDS words must not send its live partner to the fix-up kernel: it counts as in
