@@ -11,6 +11,8 @@ OBJDIR  ?= build/obj
 LIB     ?= sda_amd/libsda_engine.so
 
 GEN_PARTS    := 3 9 27 81
+# objects whose share-gen kernels stage their tiles by LDS DMA (SDA_GEN_DMA)
+GEN_DMA_PARTS ?= 27
 REVEAL_PARTS := 8 16 32 64 96
 PLAIN   := combine elementwise chacha codec snapshot packed_wide
 OBJS    := $(patsubst %,$(OBJDIR)/%.o,$(PLAIN)) $(OBJDIR)/engine.o \
@@ -26,7 +28,7 @@ $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 
 $(OBJDIR)/packed_gen_%.o: $(CSRC)/packed_gen.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) $(EXTRA) -DSDA_GEN_PART=$* -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(EXTRA) $(if $(filter $*,$(GEN_DMA_PARTS)),-DSDA_GEN_DMA=1) -DSDA_GEN_PART=$* -c $< -o $@
 
 $(OBJDIR)/packed_reveal_%.o: $(CSRC)/packed_reveal.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

@@ -137,6 +137,13 @@ constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
 #ifndef SDA_GEN_PRIO_STORE
 #define SDA_GEN_PRIO_STORE 2
 #endif
+// Tile inputs staged by LDS DMA (global_load_lds_dwordx4) instead of loads into registers + ds_write:
+// share-gen 7.01-7.02 -> 6.96-6.99 ms exact, 6.52-6.56 -> 6.44-6.48 ms canonical (profiles/r05u).  Off by
+// default; the Makefile turns it on for the N3 = 27 object only (GEN_DMA_PARTS), so the other objects keep
+// their register-stage code byte for byte ("LDS-DMA staging", has why).
+#ifndef SDA_GEN_DMA
+#define SDA_GEN_DMA 0
+#endif
 template <int LEVEL>
 __device__ __forceinline__ void set_prio() {
     if constexpr (SDA_GEN_PRIO) __builtin_amdgcn_s_setprio(LEVEL);
@@ -266,7 +273,28 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         // uniform: no tail batch, no padding (SDA_GEN_FULLTILE = 0, a build-time A/B knob, stages every tile
         // through the bounds-checked loops)
         const bool full = SDA_GEN_FULLTILE && b0 + BS <= B && (b0 + BS) * k <= D;
-        if (full) {
+        bool staged = false;
+        if constexpr (SDA_GEN_DMA && !PAD && BS == 256) {
+            // a full tile's inputs are two contiguous blocks, BS k secrets and BS t draws, laid out in LDS
+            // exactly as in HBM: global_load_lds_dwordx4 copies them straight in, 1 KiB per wave
+            // instruction, no VGPRs, no ds_write (when both blocks are 16-byte aligned)
+            const int64_t* sblk = sec + b0 * k;
+            const int64_t* dblk = draws + ((uint64_t)vec * B + b0) * t;
+            if (full && (((uintptr_t)sblk | (uintptr_t)dblk) & 15) == 0) {
+                typedef __attribute__((address_space(3))) char lds_char;
+                lds_char* lbase = (lds_char*)lds;
+                const uint32_t w = tid >> 6, l = tid & 63;
+                const uint32_t nsc = 2 * k, ndc = 2 * t;          // 1 KiB chunks: BS k * 8 / 1024 = 2 k
+                for (uint32_t c = w; c < nsc; c += BS / 64)
+                    __builtin_amdgcn_global_load_lds((const void*)(sblk + c * 128 + 2 * l), lbase + c * 1024, 16, 0, 0);
+                for (uint32_t c = w; c < ndc; c += BS / 64)
+                    __builtin_amdgcn_global_load_lds((const void*)(dblk + c * 128 + 2 * l), lbase + (nsc + c) * 1024,
+                                                     16, 0, 0);
+                staged = true;
+            }
+        }
+        if (staged) {
+        } else if (full) {
             // the tile's BS (k + t) = BS (L - 1) input words as L - 1 rows of BS: row u < k is secrets
             // [b0 k + u BS, +BS), row u >= k draws [(vec B + b0) t + (u - k) BS, +BS) -- each row one
             // coalesced load from a uniform base, landing at lds[u BS + tid] (the layout below)
