@@ -7,11 +7,21 @@
 namespace sda {
 using namespace packed;
 
-// One dispatcher per N3 = n+1; each is compiled in its own object (Makefile: -DSDA_GEN_PART=N3)
-// so the instantiations build in parallel.
-template <int N3>
-hipError_t gen_dispatch_L(uint32_t L, const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B,
-                          const GenTables* T, const GenFixupLog& log, hipStream_t s);
+// One launcher per (L = k+t+1, N3 = n+1); each is compiled in its own object (Makefile:
+// -DSDA_GEN_PART=N3 -DSDA_GEN_L=L) so the instantiations build in parallel.
+template <int L, int N3>
+hipError_t gen_launch(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
+                      const GenFixupLog& log, hipStream_t s);
+
+// Which schemes the register kernels serve (the rest run packed_wide.hip's workspace kernels).  At n + 1 = 81
+// the exact kernel without lazy truncation (p < 2^24, or odd B) needs its 64-bit sign products on top of 81
+// (sign, residue) pairs: at L >= 16 that is more than the 256 VGPRs of a wave (round 5: 335-512 registers at
+// L >= 32, 79-256 of them AGPRs used as VGPR overflow, scratch at L = 64 -- the class of kernel that faulted in
+// rounds 4 and 5; 46-74 VGPRs spilled at L = 16 even with 256).  DESIGN.md §4.2, "Register budget at
+// n + 1 = 81"; tests/test_kernel_resources.py checks every shipped code object.
+constexpr bool gen_register_path(uint32_t L, uint32_t N3, bool exact_nonlazy) {
+    return L <= 64 && N3 <= 81 && !(N3 == 81 && L >= 16 && exact_nonlazy);
+}
 
 #ifdef SDA_GEN_PART
 namespace {
@@ -138,11 +148,10 @@ constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
 #define SDA_GEN_PRIO_STORE 2
 #endif
 // Tile inputs staged by LDS DMA (global_load_lds_dwordx4) instead of loads into registers + ds_write:
-// share-gen 7.01-7.02 -> 6.96-6.99 ms exact, 6.52-6.56 -> 6.44-6.48 ms canonical (profiles/r05u).  Off by
-// default; the Makefile turns it on for the N3 = 27 object only (GEN_DMA_PARTS), so the other objects keep
-// their register-stage code byte for byte ("LDS-DMA staging", has why).
+// share-gen 7.01-7.02 -> 6.96-6.99 ms exact, 6.52-6.56 -> 6.44-6.48 ms canonical (profiles/r05u).  On in every
+// object since round 6 ("LDS-DMA staging"); SDA_GEN_DMA = 0 is the A/B knob.
 #ifndef SDA_GEN_DMA
-#define SDA_GEN_DMA 0
+#define SDA_GEN_DMA 1
 #endif
 template <int LEVEL>
 __device__ __forceinline__ void set_prio() {
@@ -150,9 +159,13 @@ __device__ __forceinline__ void set_prio() {
 }
 
 // Waves per EU: 5 where the transform fits 102 VGPRs without spilling (canonical and lazy-exact at
-// L <= 16), else SDA_GEN_WAVES (4: 128 VGPRs).
-template <int L, bool CANON, bool LAZY>
-constexpr int gen_waves() { return (L <= 16 && (CANON || LAZY)) ? 5 : SDA_GEN_WAVES; }
+// L <= 16), else SDA_GEN_WAVES (4: 128 VGPRs).  n + 1 = 81 keeps 81 shares in registers (162 VGPRs for the
+// exact kernels' (sign, residue) pairs): 2 waves, 256 VGPRs, so no instantiation spills (round 5 ran them at
+// 4-5 waves with up to 1.1 KiB of scratch per lane).
+template <int L, int N3, bool CANON, bool LAZY>
+constexpr int gen_waves() {
+    return N3 >= 81 ? 2 : (L <= 16 && (CANON || LAZY)) ? 5 : SDA_GEN_WAVES;
+}
 
 
 // CANONICAL share generation: the same transform in canonical residues [0, p) only -- no sign
@@ -231,7 +244,7 @@ __device__ __forceinline__ void transform_canon(const int64_t (&raw)[L], const G
 // words in SGPRs across tiles and spill.)
 template <int L, int N3, bool WIDE, bool CANON, bool LAZY, bool SIGNBIT = false>
 __global__ __launch_bounds__(gen_block<L>())
-__attribute__((amdgpu_waves_per_eu(gen_waves<L, CANON, LAZY>(), gen_waves<L, CANON, LAZY>())))
+__attribute__((amdgpu_waves_per_eu(gen_waves<L, N3, CANON, LAZY>(), gen_waves<L, N3, CANON, LAZY>())))
 void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const int64_t* __restrict__ draws,
                        int64_t* __restrict__ out, uint32_t k, uint32_t t, uint64_t B,
                        const GenTables* __restrict__ Tp, unsigned int* __restrict__ log, int xcd) {
@@ -250,8 +263,9 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
     const int64_t P = (int64_t)p;
     // LDS word e (batch-major [batch][k] secrets, then [batch][t] draws) lives at lpos(e): one pad
     // word per 16 keeps the even/odd lane->batch reads below 2-way bank conflicted (b64 optimum).
-    // (Unpadded at 5 waves/EU: 5 tiles of <= 31.75 KiB fit the 160 KiB LDS; the pad measured neutral.)
-    constexpr bool PAD = gen_waves<L, CANON, LAZY>() < 5;
+    // (Unpadded at 5 waves/EU: 5 tiles of <= 31.75 KiB fit the 160 KiB LDS; the pad measured neutral.  Unpadded
+    // at n + 1 = 81 too: 2 waves per EU, VALU-bound, and the layout the LDS-DMA stage needs.)
+    constexpr bool PAD = gen_waves<L, N3, CANON, LAZY>() < 5 && N3 < 81;
     __shared__ int64_t lds[BS * (L - 1) + (PAD ? BS * (L - 1) / 16 + 1 : 0)];
     auto lpos = [](uint32_t e) { return PAD ? e + (e >> 4) : e; };
 
@@ -277,19 +291,23 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
         if constexpr (SDA_GEN_DMA && !PAD && BS == 256) {
             // a full tile's inputs are two contiguous blocks, BS k secrets and BS t draws, laid out in LDS
             // exactly as in HBM: global_load_lds_dwordx4 copies them straight in, 1 KiB per wave
-            // instruction, no VGPRs, no ds_write (when both blocks are 16-byte aligned)
+            // instruction, no VGPRs, no ds_write (when both blocks are 16-byte aligned).  One loop over the
+            // 2 (k + t) chunks with a computed source and a wave-uniform chunk index: every DMA of the tile is
+            // issued before any wait (round 5's two loops put an s_waitcnt vmcnt(0) between them).
             const int64_t* sblk = sec + b0 * k;
             const int64_t* dblk = draws + ((uint64_t)vec * B + b0) * t;
             if (full && (((uintptr_t)sblk | (uintptr_t)dblk) & 15) == 0) {
                 typedef __attribute__((address_space(3))) char lds_char;
                 lds_char* lbase = (lds_char*)lds;
-                const uint32_t w = tid >> 6, l = tid & 63;
-                const uint32_t nsc = 2 * k, ndc = 2 * t;          // 1 KiB chunks: BS k * 8 / 1024 = 2 k
-                for (uint32_t c = w; c < nsc; c += BS / 64)
-                    __builtin_amdgcn_global_load_lds((const void*)(sblk + c * 128 + 2 * l), lbase + c * 1024, 16, 0, 0);
-                for (uint32_t c = w; c < ndc; c += BS / 64)
-                    __builtin_amdgcn_global_load_lds((const void*)(dblk + c * 128 + 2 * l), lbase + (nsc + c) * 1024,
-                                                     16, 0, 0);
+                const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
+                const uint32_t nsc = 2 * k, nc = 2 * (k + t);    // 1 KiB chunks: BS k * 8 / 1024 = 2 k
+                for (uint32_t c = w; c < nc; c += BS / 64) {
+                    const int64_t* src = c < nsc ? sblk + (uint64_t)c * 128 : dblk + (uint64_t)(c - nsc) * 128;
+                    __builtin_amdgcn_global_load_lds((const void*)(src + 2 * l), lbase + c * 1024, 16, 0, 0);
+                }
+                // the LDS writes of a DMA count in vmcnt, and s_barrier does not wait for them: every wave drains
+                // its own DMAs before the barrier, so the other waves' reads see every chunk
+                __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0) (gfx9 encoding; lgkm/exp counters untouched)
                 staged = true;
             }
         }
@@ -555,53 +573,45 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
 
 }  // namespace
 
+// The non-lazy exact kernels (p < 2^24, or odd B / unaligned out) exist only where gen_register_path admits them.
 template <int L, int N3, bool CANON>
-static void gen_launch_mode(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
-                            uint32_t p, const GenFixupLog& log, hipStream_t s) {
+static hipError_t gen_launch_mode(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
+                                  uint32_t p, const GenFixupLog& log, hipStream_t s) {
     constexpr int BS = gen_block<L>();
     const dim3 grid((unsigned)((B + BS - 1) / BS), (unsigned)a.n_vectors);
     const bool wide = B % 2 == 0 && ((uintptr_t)a.out % 16) == 0;
     const int xcd = a.xcd_order && (uint64_t)grid.x * grid.y < (1ull << 32) ? 1 : 0;
+    constexpr bool NONLAZY = CANON || gen_register_path(L, N3, true);
     if (wide && !CANON && p >= kLazyTruncMinP && a.signbit)   // exact shares, sign-bit radix-2 half
         hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, false, true, true>), grid, dim3(BS), 0, s, a.secrets,
                            a.dimension, a.draws, a.out, k, t, B, T, log.count, xcd);
     else if (wide && !CANON && p >= kLazyTruncMinP)          // exact shares, lazy zero handling
         hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, false, true>), grid, dim3(BS), 0, s, a.secrets,
                            a.dimension, a.draws, a.out, k, t, B, T, log.count, xcd);
+    else if constexpr (!NONLAZY)
+        return hipErrorInvalidValue;                          // the dispatcher sends these to packed_wide.hip
     else if (wide)
         hipLaunchKernelGGL((packed_gen_kernel<L, N3, true, CANON, false>), grid, dim3(BS), 0, s, a.secrets,
                            a.dimension, a.draws, a.out, k, t, B, T, log.count, xcd);
     else
         hipLaunchKernelGGL((packed_gen_kernel<L, N3, false, CANON, false>), grid, dim3(BS), 0, s, a.secrets,
                            a.dimension, a.draws, a.out, k, t, B, T, log.count, xcd);
+    return hipSuccess;
 }
 
 template <int L, int N3>
-static hipError_t gen_launch(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
-                             const GenFixupLog& log, hipStream_t s) {
+hipError_t gen_launch(const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B, const GenTables* T,
+                      const GenFixupLog& log, hipStream_t s) {
     constexpr int BS = gen_block<L>();
     if ((B + BS - 1) / BS > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const uint32_t p = a.prime;
-    if (a.canonical) gen_launch_mode<L, N3, true>(a, k, t, B, T, p, log, s);
-    else gen_launch_mode<L, N3, false>(a, k, t, B, T, p, log, s);
+    const hipError_t e = a.canonical ? gen_launch_mode<L, N3, true>(a, k, t, B, T, p, log, s)
+                                     : gen_launch_mode<L, N3, false>(a, k, t, B, T, p, log, s);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
-
-template <int N3>
-hipError_t gen_dispatch_L(uint32_t L, const PackedGenArgs& a, uint32_t k, uint32_t t, uint64_t B,
-                          const GenTables* T, const GenFixupLog& log, hipStream_t s) {
-    switch (L) {
-        case 2: return gen_launch<2, N3>(a, k, t, B, T, log, s);
-        case 4: if constexpr (N3 >= 4) return gen_launch<4, N3>(a, k, t, B, T, log, s); break;
-        case 8: if constexpr (N3 >= 8) return gen_launch<8, N3>(a, k, t, B, T, log, s); break;
-        case 16: if constexpr (N3 >= 16) return gen_launch<16, N3>(a, k, t, B, T, log, s); break;
-        case 32: if constexpr (N3 >= 32) return gen_launch<32, N3>(a, k, t, B, T, log, s); break;
-        case 64: if constexpr (N3 >= 64) return gen_launch<64, N3>(a, k, t, B, T, log, s); break;
-    }
-    return hipErrorInvalidValue;
-}
-template hipError_t gen_dispatch_L<SDA_GEN_PART>(uint32_t, const PackedGenArgs&, uint32_t, uint32_t, uint64_t,
-                                                 const GenTables*, const GenFixupLog&, hipStream_t);
+template hipError_t gen_launch<SDA_GEN_L, SDA_GEN_PART>(const PackedGenArgs&, uint32_t, uint32_t, uint64_t,
+                                                        const GenTables*, const GenFixupLog&, hipStream_t);
 
 #else  // dispatcher, tables, generic fix-up
 
@@ -705,9 +715,11 @@ hipError_t launch_packed_generate(const PackedGenArgs& args, uint32_t k, uint32_
     PackedGenArgs a = args;
     a.prime = p;
     const uint32_t L = k + t + 1, N3 = n + 1;
-    if (L > 64 || N3 > 81)                       // past the register kernels: packed_wide.hip
-        return launch_packed_generate_wide(a, k, t, n, p, omega_secrets, omega_shares, tab, s);
     const uint64_t B = (a.dimension + k - 1) / k;
+    // the register kernels' variant: WIDE stores need even B and 16-byte aligned out; lazy truncation p >= 2^24
+    const bool exact_nonlazy = !a.canonical && !(B % 2 == 0 && ((uintptr_t)a.out % 16) == 0 && p >= kLazyTruncMinP);
+    if (!gen_register_path(L, N3, exact_nonlazy))            // past the register kernels: packed_wide.hip
+        return launch_packed_generate_wide(a, k, t, n, p, omega_secrets, omega_shares, tab, s);
     if (B == 0 || a.n_vectors == 0) return hipSuccess;
     const uint32_t kv[5] = {L, N3, p, omega_secrets, omega_shares};
     std::vector<uint8_t> key((const uint8_t*)kv, (const uint8_t*)kv + sizeof(kv));
@@ -727,11 +739,14 @@ hipError_t launch_packed_generate(const PackedGenArgs& args, uint32_t k, uint32_
                     reinterpret_cast<uint64_t*>(static_cast<unsigned int*>(log_buf) + 16), kGenLogCap};
     hipError_t e = hipMemsetAsync(log.count, 0, sizeof(unsigned int), s);
     if (e != hipSuccess) return e;
-    switch (N3) {
-        case 3: e = gen_dispatch_L<3>(L, a, k, t, B, T, log, s); break;
-        case 9: e = gen_dispatch_L<9>(L, a, k, t, B, T, log, s); break;
-        case 27: e = gen_dispatch_L<27>(L, a, k, t, B, T, log, s); break;
-        case 81: e = gen_dispatch_L<81>(L, a, k, t, B, T, log, s); break;
+    switch (N3 * 128 + L) {             // one object per (N3, L): Makefile GEN_PARTS
+#define SDA_GEN_CASE(N, LL) case N * 128 + LL: e = gen_launch<LL, N>(a, k, t, B, T, log, s); break;
+        SDA_GEN_CASE(3, 2)
+        SDA_GEN_CASE(9, 2) SDA_GEN_CASE(9, 4) SDA_GEN_CASE(9, 8)
+        SDA_GEN_CASE(27, 2) SDA_GEN_CASE(27, 4) SDA_GEN_CASE(27, 8) SDA_GEN_CASE(27, 16)
+        SDA_GEN_CASE(81, 2) SDA_GEN_CASE(81, 4) SDA_GEN_CASE(81, 8) SDA_GEN_CASE(81, 16) SDA_GEN_CASE(81, 32)
+        SDA_GEN_CASE(81, 64)
+#undef SDA_GEN_CASE
         default: e = hipErrorInvalidValue;
     }
     if (e != hipSuccess) return e;

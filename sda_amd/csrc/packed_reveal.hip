@@ -1,4 +1,6 @@
 // packed_reveal.hip -- packed-Shamir reveal, EXACT (Newton) and CANONICAL (Lagrange).
+#include <algorithm>
+
 #include "packed_common.h"
 #include "xcd.h"
 
@@ -283,7 +285,7 @@ __device__ void reveal_exact_generic(const int64_t* __restrict__ sh, uint64_t B,
 // log overflowed, every batch of the launch is recomputed (correct and slow; only reachable with raw
 // i64 shares).  One wave per workgroup: a logged batch is rare, so few lanes are busy.
 template <int MMAX, int KU>
-__global__ __launch_bounds__(64) void packed_reveal_fixup_kernel(const int64_t* __restrict__ shares, uint64_t B,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void packed_reveal_fixup_kernel(const int64_t* __restrict__ shares, uint64_t B,
                                                                  uint64_t D, uint64_t n_vec, int64_t* __restrict__ out,
                                                                  uint32_t n_idx, uint32_t k,
                                                                  const uint32_t* __restrict__ tab, MontP M,
@@ -338,7 +340,7 @@ __device__ __forceinline__ int32_t trem_small(int64_t v, uint32_t p) {
 // trem_prod; otherwise (raw i64 shares) the generic i64 arithmetic.  A trapped batch is a serial
 // latency chain for one lane on the register path (~40 us); spread over the wave it is m + k short steps.
 template <int MMAX>
-__global__ __launch_bounds__(64) void packed_reveal_fixup_wave_kernel(const int64_t* __restrict__ shares, uint64_t B,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void packed_reveal_fixup_wave_kernel(const int64_t* __restrict__ shares, uint64_t B,
                                                                       uint64_t D, uint64_t n_vec,
                                                                       int64_t* __restrict__ out, uint32_t n_idx,
                                                                       uint32_t k, const uint32_t* __restrict__ tab,
@@ -353,12 +355,27 @@ __global__ __launch_bounds__(64) void packed_reveal_fixup_wave_kernel(const int6
     const uint32_t m = n_idx + 1, lane = threadIdx.x;
     const Mod64 P = make_mod64((int64_t)p);
     const double pinv = 1.0 / (double)p;
-    int32_t inv[MMAX], np[MMAX];          // this lane's inv[j][lane] and np[lane][i]
+    // this lane's inv[j][lane] and np[lane][i]: in registers up to 16 points; past that in LDS (2 x 16 KiB), so
+    // the 32- and 64-point instantiations stay inside 256 VGPRs (round 5 held both tables in registers: 274 and
+    // 376 registers, AGPRs standing in for VGPRs -- tests/test_kernel_resources.py)
+    constexpr bool REG = MMAX <= 16;
+    constexpr int RT = REG ? MMAX : 1;
+    int32_t inv_r[RT], np_r[RT];
+    __shared__ int32_t tabs[REG ? 1 : 2 * MMAX * 64];
+    auto inv = [&](int j) -> int32_t {
+        if constexpr (REG) return inv_r[j]; else return tabs[j * 64 + lane];
+    };
+    auto np = [&](int i) -> int32_t {
+        if constexpr (REG) return np_r[i]; else return tabs[(MMAX + i) * 64 + lane];
+    };
 #pragma unroll
     for (int j = 0; j < MMAX; ++j) {
-        inv[j] = (j >= 1 && lane < MMAX) ? (int32_t)tab[OFF_INV + j * TS + (lane < MMAX ? lane : 0)] : 0;
-        np[j] = lane < k ? (int32_t)tab[OFF_NP + (lane < k ? lane : 0) * TS + j] : 0;
+        const int32_t iv = (j >= 1 && lane < MMAX) ? (int32_t)tab[OFF_INV + j * TS + (lane < MMAX ? lane : 0)] : 0;
+        const int32_t nv = lane < k ? (int32_t)tab[OFF_NP + (lane < k ? lane : 0) * TS + j] : 0;
+        if constexpr (REG) { inv_r[j] = iv; np_r[j] = nv; }
+        else { tabs[j * 64 + lane] = iv; tabs[(MMAX + j) * 64 + lane] = nv; }
     }
+    if constexpr (!REG) __syncthreads();
     for (uint64_t w = blockIdx.x; w < total; w += gridDim.x) {
         const uint64_t gb = all ? w : list[w];
         const uint64_t vec = gb / B, b = gb - vec * B;
@@ -373,13 +390,13 @@ __global__ __launch_bounds__(64) void packed_reveal_fixup_wave_kernel(const int6
             for (int j = 1; j < MMAX; ++j) {
                 const int32_t prev = __shfl_up(x, 1);
                 if ((uint32_t)j < m && lane >= (uint32_t)j && lane < m)
-                    x = (int32_t)trem_prod(trem_small((int64_t)x - prev, p), inv[j], p, pinv);
+                    x = (int32_t)trem_prod(trem_small((int64_t)x - prev, p), inv(j), p, pinv);
             }
             int32_t a = 0;
 #pragma unroll
             for (int i = 0; i < MMAX; ++i) {
                 const int32_t c = __shfl(x, i);
-                if ((uint32_t)i < m) a = trem_small((int64_t)a + trem_prod(c, np[i], p, pinv), p);
+                if ((uint32_t)i < m) a = trem_small((int64_t)a + trem_prod(c, np(i), p, pinv), p);
             }
             acc = a;
         } else {
@@ -387,12 +404,12 @@ __global__ __launch_bounds__(64) void packed_reveal_fixup_wave_kernel(const int6
             for (int j = 1; j < MMAX; ++j) {
                 const int64_t prev = __shfl_up(s, 1);
                 if ((uint32_t)j < m && lane >= (uint32_t)j && lane < m)
-                    s = trem64(wmul(trem64(wsub(s, prev), P), inv[j]), P);
+                    s = trem64(wmul(trem64(wsub(s, prev), P), inv(j)), P);
             }
 #pragma unroll
             for (int i = 0; i < MMAX; ++i) {
                 const int64_t c = __shfl(s, i);
-                if ((uint32_t)i < m) acc = trem64(wadd(acc, trem64(wmul(c, np[i]), P)), P);
+                if ((uint32_t)i < m) acc = trem64(wadd(acc, trem64(wmul(c, np(i)), P)), P);
             }
         }
         if (lane < lim) out[vec * D + b * k + lane] = acc;                     // batched.rs:94
@@ -426,7 +443,7 @@ __global__ __launch_bounds__(256) void packed_reveal_canon_kernel(const int64_t*
         in_range = in_range && ((uint32_t)i >= n_idx || (uint64_t)(v + (P - 1)) < (uint64_t)(2 * P - 1));
         S[i] = (uint32_t)i < n_idx ? canon32((int32_t)v, p) : 0u;
     };
-    if constexpr (NMAX <= 64) {          // every load first (all in flight), then convert
+    if constexpr (NMAX <= 32) {          // every load first (all in flight), then convert
         int64_t v[NMAX];
         static_for<0, NMAX>([&](auto i) { v[i] = sh[(uint64_t)((uint32_t)i < n_idx ? i : 0) * B]; });
         static_for<0, NMAX>([&](auto i) { take(i, v[i]); });
@@ -499,13 +516,15 @@ hipError_t reveal_launch(int mode, const PackedRevealArgs& a, uint64_t B, uint32
         } else
             hipLaunchKernelGGL((packed_reveal_fixup_kernel<MM, 0>), dim3(64), dim3(64), 0, s, a.shares, B,
                                a.dimension, a.n_vectors, a.out, n_idx, k, tab, M, log);
-    } else {
+    } else if constexpr (MM <= 32) {
         if (staged)
             hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, true>), grid, dim3(256), lds, s, a.shares, B,
                                a.dimension, a.out, n_idx, k, tab, M, xcd);
         else
             hipLaunchKernelGGL((packed_reveal_canon_kernel<MM, false>), grid, dim3(256), 0, s, a.shares, B,
                                a.dimension, a.out, n_idx, k, tab, M, xcd);
+    } else {
+        return hipErrorInvalidValue;                  // launch_packed_reveal runs these as exact + canonical
     }
     return hipGetLastError();
 }
@@ -565,6 +584,24 @@ hipError_t launch_packed_reveal(const PackedRevealArgs& a, const uint64_t* indic
     if (B == 0 || a.n_vectors == 0) return hipSuccess;
     if ((mode == 0 ? n_idx + 1 : n_idx) > (uint32_t)kRevealMaxPoints || k > (uint32_t)KMAX)   // packed_wide.hip
         return launch_packed_reveal_wide(a, indices, n_idx, k, p, omega_secrets, omega_shares, mode, tab, s);
+    if (mode == 1 && n_idx > 32) {
+        // CANONICAL from more than 32 shares: the exact Newton kernels, then one canonicalising pass -- the same
+        // values by definition (CANONICAL = positive() of the exact reveal, as on the workspace path).  The
+        // Lagrange kernel's 64- and 96-point instantiations needed AGPRs standing in for VGPRs, or scratch
+        // (tests/test_kernel_resources.py; DESIGN.md §4.2 "Register budget at n + 1 = 81").
+        std::vector<int64_t> pts(n_idx);
+        for (uint32_t i = 0; i < n_idx; ++i) pts[i] = h_powmod(omega_shares, (uint32_t)(indices[i] + 1), p);
+        std::sort(pts.begin(), pts.end());
+        if (std::adjacent_find(pts.begin(), pts.end()) != pts.end() || pts[0] == 1)
+            return hipErrorInvalidValue;              // repeated points: no Lagrange form (as the canonical tables)
+        const uint32_t m = n_idx + 1;
+        hipError_t e = m > (uint32_t)kRevealMaxPoints
+                           ? launch_packed_reveal_wide(a, indices, n_idx, k, p, omega_secrets, omega_shares, 1, tab, s)
+                           : launch_packed_reveal(a, indices, n_idx, k, p, omega_secrets, omega_shares, 0, tab,
+                                                  log_buf, s);
+        if (e != hipSuccess || m > (uint32_t)kRevealMaxPoints) return e;
+        return launch_mod_canonical(a.out, a.dimension * a.n_vectors, a.out, p, s);
+    }
     std::vector<uint8_t> key(sizeof(uint32_t) * 6 + sizeof(uint64_t) * n_idx);
     const uint32_t kv[6] = {n_idx, k, p, omega_secrets, omega_shares, (uint32_t)mode};
     memcpy(key.data(), kv, sizeof(kv));
