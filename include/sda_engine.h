@@ -8,8 +8,12 @@
  * and client/src/crypto/masking/mod.rs:33-94.
  *
  * Conventions
- *   - Host entry points stream their inputs through pinned double buffers in row tiles of
+ *   - sda_share_combine, the Full sda_mask_combine, the Additive sda_secret_reconstruct and
+ *     sda_clerk_decode_combine stream their inputs through pinned double buffers in row tiles of
  *     SDA_HOST_STAGE_MB (default 256) MiB, so a job larger than HBM runs (bit-identical to one pass).
+ *     The other host entry points (packed and additive generate, packed reconstruct, ChaCha mask
+ *     combine, sda_recipient_reveal) stage their whole job -- or, on a multi-device handle, each
+ *     device's share of it -- in device memory, and return OUT_OF_MEMORY past it.
  *   - Elements are i64 (client/src/crypto/mod.rs:33-36); arithmetic follows
  *     Rust: truncated `%`, wrapping `+` (release builds).
  *   - The caller owns every buffer.  Host entry points are synchronous (they
@@ -353,21 +357,26 @@ sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64
 /* HBM for the resident hot-path buffers (no reference counterpart: the reference's buffers are Rust
  * Vec<i64> on the host, batched.rs:25-28).  `bytes` of device memory on `device`, one virtual range
  * mapped from physical chunks of SDA_HBM_CHUNK_MB (default 64) MiB, so its backing never depends on how
- * fragmented the driver's free VRAM is.  The range is rounded up to whole chunks.
+ * fragmented the driver's free VRAM is.  The request is rounded up to whole chunks, and
+ * belongs to a size class (n chunks: n up to 4, then 4..7 x 2^e, at most 25 % more): the buffer reserves
+ * its class's virtual range and maps the chunks asked for.
  * sda_hbm_free does not wait: the buffer returns to a per-process pool, still mapped, and a later
- * sda_hbm_alloc of up to its size (and at least half of it) gets it back (after a device-wide sync if it
- * was freed since the allocator's last one).  The pool holds at most SDA_HBM_POOL_MB (default 32768) MiB
- * per device: sda_hbm_alloc trims the oldest pooled buffers down to that bound first, and trims the whole
- * pool and retries once when the device is out of memory.  Trimming syncs the device and releases the
- * physical chunks; the virtual range stays reserved and is never mapped again (DESIGN.md §2 gives the
- * cause).  NULL is a no-op; a pointer not returned by sda_hbm_alloc, or freed twice, is INVALID_ARGUMENT. */
+ * sda_hbm_alloc of the same size class gets it back (after a device-wide sync if none has completed since
+ * the free; extra chunks, if it needs more, are mapped at the range's never-mapped tail).  The pool holds
+ * at most SDA_HBM_POOL_MB (default 32768) MiB per device: an allocation that finds no pooled buffer of its
+ * class trims the oldest pooled buffers down to that bound, and trims the whole pool and retries once when
+ * the device is out of memory.  Trimming syncs the device and releases the physical chunks; the virtual
+ * range stays reserved and is never mapped again (DESIGN.md §2 gives the cause).  NULL is a no-op; a
+ * pointer not returned by sda_hbm_alloc, or freed twice, is INVALID_ARGUMENT.  Thread-safe; no lock is
+ * held across a device sync. */
 sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out);
 sda_status sda_hbm_free(void* ptr);
 /* Release pooled buffers of `device` (oldest first) until at most keep_bytes stay pooled.
- * sda_engine_destroy trims its device's pool to 0. */
+ * Destroying the last live engine handle of a device trims that device's pool to 0. */
 sda_status sda_hbm_trim(int device, uint64_t keep_bytes);
-/* Bytes of `device` handed out, pooled (freed, mapped) and retired (virtual ranges kept reserved after a
- * trim); any pointer may be NULL. */
+/* Bytes of `device` handed out and pooled (mapped chunks), and retired (virtual ranges kept reserved
+ * after a trim; a steady stream of jobs whose buffers fit the pool retires none); any pointer may be
+ * NULL. */
 sda_status sda_hbm_stats(int device, uint64_t* live_bytes, uint64_t* pooled_bytes, uint64_t* retired_bytes);
 
 #ifdef __cplusplus

@@ -135,6 +135,8 @@ bool scratch_hbm(size_t bytes) {
     return on && bytes >= kScratchHbmMin;
 }
 bool hbm_owned(void* p);      // (HBM section) p was returned by sda_hbm_alloc and not freed
+void hbm_engine_opened(int device);   // (HBM section) live engine handles per device
+bool hbm_engine_closed(int device);   // true when that was the device's last live handle
 
 void dev_free(void* p) {
     if (!p) return;
@@ -381,6 +383,7 @@ sda_status sda_engine_create(int device_ordinal, sda_engine** out) {
         return fail(SDA_ERR_DEVICE, "hipStreamCreate/hipEventCreate: %s", hipGetErrorString(e));
     }
     h->last_stream = h->stream;
+    hbm_engine_opened(device_ordinal);
     *out = h;
     return ok();
 }
@@ -415,7 +418,9 @@ void sda_engine_destroy(sda_engine* h) {
     if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
     if (h->order_ev) (void)hipEventDestroy(h->order_ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
-    (void)sda_hbm_trim(h->device, 0);        // the device's pooled sda_hbm_alloc buffers go back to the driver
+    // the device's last engine handle gives its pooled sda_hbm_alloc buffers back to the driver (with other
+    // handles alive, buffers they or torch freed stay pooled for them)
+    if (hbm_engine_closed(h->device)) (void)sda_hbm_trim(h->device, 0);
     delete h;
 }
 
@@ -900,14 +905,19 @@ sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64
 // shuffled (profiles/r04r).  sda_hbm_alloc / sda_hbm_free give the resident hot-path buffers that backing.
 //
 // Life cycle ("HBM backing"):
-//   - sda_hbm_free never waits: the buffer goes to a per-process pool, still mapped, stamped with the
-//     device's sync epoch.  Work queued on any stream may still use it.  (SDA_HBM_POOL_MB=0 disables the
-//     pool: free then syncs the device and releases the buffer at once.)
-//   - sda_hbm_alloc hands out the smallest pooled buffer that fits (at most twice the size asked for); one
-//     freed since the last device-wide sync costs a hipDeviceSynchronize first.
-//   - The pool is bounded: SDA_HBM_POOL_MB (default 32768) per device.  An allocation first trims the
-//     oldest pooled buffers down to the bound; an allocation that hits OUT_OF_MEMORY trims the whole pool
-//     and retries once; sda_hbm_trim and sda_engine_destroy trim explicitly.
+//   - Size classes.  A request of n chunks belongs to class cls(n): n itself up to 4 chunks, then 4..7 x 2^e
+//     (at most 25 % above n).  A buffer reserves its class's whole virtual range but maps only the chunks
+//     asked for; a later request of the same class reuses it and maps more chunks at the range's never-mapped
+//     tail if it needs them.  So a steady stream of jobs -- same sizes or mixed -- finds its buffers in the
+//     pool and never trims (tests/abi_c/hbm_cycle.c: 10,000 alloc/free cycles of mixed sizes, nothing retired).
+//   - sda_hbm_free never waits: the buffer goes to a per-process pool, still mapped, stamped with the number
+//     of device-wide syncs the allocator had begun.  Work queued on any stream may still use it; a reuse
+//     waits for one sync begun after the free (hipDeviceSynchronize, outside the allocator's lock).
+//     (SDA_HBM_POOL_MB=0 disables the pool: free then syncs the device and releases the buffer at once.)
+//   - The pool is bounded: SDA_HBM_POOL_MB (default 32768) per device.  An allocation that finds no pooled
+//     buffer of its class first trims the oldest pooled buffers down to that bound; one that hits
+//     OUT_OF_MEMORY trims the whole pool and retries once.  sda_hbm_trim trims explicitly, and the last engine
+//     handle of a device trims its pool when it is destroyed.
 //   - Trimming syncs the device, unmaps the chunks and releases them (the HBM returns to the driver), but
 //     the VIRTUAL range stays reserved, retired, for the life of the process: it is never mapped again.
 //     Cause (profiles/r05b/hbm_repro_suite_sequence.txt): when a freed range was also returned with
@@ -916,25 +926,29 @@ sda_status sda_synth_fill_dev(sda_engine* h, int64_t* dst, uint64_t rows, uint64
 //     torch kernels, freed, the same size allocated at once) `fill_(-1)` followed by `max()` read 0s (twice out
 //     of twice), as r04y's share-gen buffer read back a different zero count on every read.  With the range
 //     retired the same sequence passes (twice out of twice), as does the whole suite.  Retired ranges cost
-//     only address space (2^47 bytes of it per process).  SDA_HBM_VA_FREE=1 restores the address free for
-//     that A/B (scripts/hbm_repro.sh).
+//     only address space (2^47 bytes of it per process), and only trims retire any (sda_hbm_stats counts it).
+//     SDA_HBM_VA_FREE=1 restores the address free for that A/B (scripts/hbm_repro.sh).
 namespace {
 
 struct HbmBuffer {
     int device = 0;
-    size_t bytes = 0;                                   // reserved (a whole number of chunks)
     size_t chunk = 0;
-    std::vector<hipMemGenericAllocationHandle_t> chunks;
-    uint64_t freed_epoch = 0;                           // pool only: the device's sync epoch at free time
+    size_t cls = 0;                                     // reserved chunks (the size class)
+    std::vector<hipMemGenericAllocationHandle_t> chunks;   // mapped chunks, from the range's start
+    uint64_t freed_ticket = 0;                          // pool only: device syncs begun at free time
     uint64_t freed_seq = 0;                             // pool only: free order (oldest is trimmed first)
+    size_t mapped_bytes() const { return chunks.size() * chunk; }
+    size_t reserved_bytes() const { return cls * chunk; }
 };
 std::mutex g_hbm_mu;
 std::map<uintptr_t, HbmBuffer> g_hbm;                   // handed out
 std::map<uintptr_t, HbmBuffer> g_hbm_pool;              // freed, still mapped
 constexpr int kHbmMaxDev = 64;
-uint64_t g_hbm_epoch[kHbmMaxDev];                       // device-wide syncs done by the allocator
+uint64_t g_hbm_sync_begun[kHbmMaxDev];                  // device-wide syncs the allocator has begun ...
+uint64_t g_hbm_sync_done[kHbmMaxDev];                   // ... and the highest such id that has completed
 uint64_t g_hbm_retired[kHbmMaxDev];                     // bytes of virtual ranges retired (never remapped)
 uint64_t g_hbm_seq = 0;
+int g_engines[kHbmMaxDev];                              // live engine handles per device (destroy-time trim)
 
 size_t hbm_chunk_bytes() {
     const char* e = getenv("SDA_HBM_CHUNK_MB");
@@ -953,17 +967,47 @@ bool hbm_va_free() {
     return e && atoi(e) == 1;
 }
 
-// unmap and release the first `mapped_chunks` chunks' mappings and every chunk handle; the virtual range is
-// retired (kept reserved) unless SDA_HBM_VA_FREE=1.  The caller has made sure no queued work uses it.
-void hbm_release(void* ptr, HbmBuffer& b, size_t mapped_chunks) {
-    for (size_t i = 0; i < mapped_chunks; ++i) (void)hipMemUnmap(static_cast<char*>(ptr) + i * b.chunk, b.chunk);
+// the size class of a request of n chunks: n up to 4, then the next 4..7 x 2^e (at most 25 % more)
+size_t hbm_class(size_t n) {
+    if (n <= 4) return n;
+    size_t e = 0;
+    while ((n >> e) >= 8) ++e;                          // n in [4, 8) x 2^e
+    const size_t m = (n + ((size_t)1 << e) - 1) >> e;  // ceil(n / 2^e) in 4..8
+    return m << e;
+}
+
+// One device-wide sync, outside the allocator's lock: afterwards every buffer freed before it began is idle.
+hipError_t hbm_sync(int device) {
+    uint64_t id;
+    {
+        std::lock_guard<std::mutex> lk(g_hbm_mu);
+        id = ++g_hbm_sync_begun[device];
+    }
+    const hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_hbm_mu);
+        if (id > g_hbm_sync_done[device]) g_hbm_sync_done[device] = id;
+    }
+    return e;
+}
+
+bool hbm_idle(const HbmBuffer& b) {   // g_hbm_mu held: a sync begun after its free has completed
+    return g_hbm_sync_done[b.device] > b.freed_ticket;
+}
+
+// unmap and release the buffer's chunks; the virtual range is retired (kept reserved) unless
+// SDA_HBM_VA_FREE=1.  The caller owns the buffer and has made sure no queued work uses it.
+void hbm_release(void* ptr, HbmBuffer& b) {
+    for (size_t i = 0; i < b.chunks.size(); ++i) (void)hipMemUnmap(static_cast<char*>(ptr) + i * b.chunk, b.chunk);
     for (auto& c : b.chunks) (void)hipMemRelease(c);
     b.chunks.clear();
     if (!ptr) return;
-    if (hbm_va_free())
-        (void)hipMemAddressFree(ptr, b.bytes);
-    else if (b.device >= 0 && b.device < kHbmMaxDev)
-        g_hbm_retired[b.device] += b.bytes;
+    if (hbm_va_free()) {
+        (void)hipMemAddressFree(ptr, b.reserved_bytes());
+    } else {
+        std::lock_guard<std::mutex> lk(g_hbm_mu);
+        g_hbm_retired[b.device] += b.reserved_bytes();
+    }
 }
 
 bool hbm_owned(void* p) {
@@ -971,64 +1015,99 @@ bool hbm_owned(void* p) {
     return g_hbm.count(reinterpret_cast<uintptr_t>(p)) != 0;
 }
 
+void hbm_engine_opened(int device) {
+    std::lock_guard<std::mutex> lk(g_hbm_mu);
+    if (device >= 0 && device < kHbmMaxDev) ++g_engines[device];
+}
+
+bool hbm_engine_closed(int device) {
+    std::lock_guard<std::mutex> lk(g_hbm_mu);
+    return device >= 0 && device < kHbmMaxDev && --g_engines[device] == 0;
+}
+
 uint64_t hbm_pooled_bytes(int device) {   // g_hbm_mu held
     uint64_t s = 0;
     for (auto& kv : g_hbm_pool)
-        if (kv.second.device == device) s += kv.second.bytes;
+        if (kv.second.device == device) s += kv.second.mapped_bytes();
     return s;
 }
 
-// Trim the device's pool (oldest first) until at most `keep` bytes stay pooled.  g_hbm_mu held; the
-// device is current.  One device-wide sync covers every buffer trimmed.
-hipError_t hbm_trim_locked(int device, uint64_t keep) {
-    uint64_t pooled = hbm_pooled_bytes(device);
-    if (pooled <= keep) return hipSuccess;
-    hipError_t e = hipDeviceSynchronize();
-    if (e != hipSuccess) return e;
-    ++g_hbm_epoch[device];
-    while (pooled > keep) {
-        auto old = g_hbm_pool.end();
-        for (auto it = g_hbm_pool.begin(); it != g_hbm_pool.end(); ++it)
-            if (it->second.device == device && (old == g_hbm_pool.end() || it->second.freed_seq < old->second.freed_seq))
-                old = it;
-        if (old == g_hbm_pool.end()) break;
-        pooled -= old->second.bytes;
-        hbm_release(reinterpret_cast<void*>(old->first), old->second, old->second.chunks.size());
-        g_hbm_pool.erase(old);
+// Trim the device's pool (oldest first) until at most `keep` bytes stay pooled.  The victims leave the pool
+// under the lock; the sync (when one of them may still be in use) and the unmapping run outside it.  The
+// device is current.
+hipError_t hbm_trim(int device, uint64_t keep) {
+    std::vector<std::pair<uintptr_t, HbmBuffer>> victims;
+    bool busy = false;
+    {
+        std::lock_guard<std::mutex> lk(g_hbm_mu);
+        uint64_t pooled = hbm_pooled_bytes(device);
+        while (pooled > keep) {
+            auto old = g_hbm_pool.end();
+            for (auto it = g_hbm_pool.begin(); it != g_hbm_pool.end(); ++it)
+                if (it->second.device == device &&
+                    (old == g_hbm_pool.end() || it->second.freed_seq < old->second.freed_seq))
+                    old = it;
+            if (old == g_hbm_pool.end()) break;
+            pooled -= old->second.mapped_bytes();
+            busy = busy || !hbm_idle(old->second);
+            victims.emplace_back(old->first, std::move(old->second));
+            g_hbm_pool.erase(old);
+        }
     }
+    if (victims.empty()) return hipSuccess;
+    hipError_t e = busy ? hbm_sync(device) : hipSuccess;
+    if (e != hipSuccess) {                               // keep them pooled (nothing was unmapped)
+        std::lock_guard<std::mutex> lk(g_hbm_mu);
+        for (auto& v : victims) g_hbm_pool[v.first] = std::move(v.second);
+        return e;
+    }
+    for (auto& v : victims) hbm_release(reinterpret_cast<void*>(v.first), v.second);
     return hipSuccess;
 }
 
-// Reserve + map a new buffer of n chunks.
-hipError_t hbm_create(int device, size_t n, size_t chunk, const hipMemAllocationProp& prop, void** out, HbmBuffer* b) {
-    b->device = device;
-    b->bytes = n * chunk;
-    b->chunk = chunk;
-    void* ptr = nullptr;
-    hipError_t e = hipMemAddressReserve(&ptr, b->bytes, chunk, nullptr, 0);
-    if (e != hipSuccess) return e;
-    b->chunks.reserve(n);
-    size_t mapped = 0;
-    for (size_t i = 0; i < n && e == hipSuccess; ++i) {
+// Map chunks [b.chunks.size(), n) of the buffer's reserved range: fresh chunks at a never-mapped tail.
+hipError_t hbm_map_to(void* ptr, HbmBuffer* b, size_t n, const hipMemAllocationProp& prop) {
+    const size_t m0 = b->chunks.size();
+    hipError_t e = hipSuccess;
+    for (size_t i = m0; i < n && e == hipSuccess; ++i) {
         hipMemGenericAllocationHandle_t c;
-        e = hipMemCreate(&c, chunk, &prop, 0);
+        e = hipMemCreate(&c, b->chunk, &prop, 0);
         if (e != hipSuccess) break;
+        e = hipMemMap(static_cast<char*>(ptr) + i * b->chunk, b->chunk, 0, c, 0);
+        if (e != hipSuccess) {
+            (void)hipMemRelease(c);
+            break;
+        }
         b->chunks.push_back(c);
-        e = hipMemMap(static_cast<char*>(ptr) + i * chunk, chunk, 0, c, 0);
-        if (e == hipSuccess) ++mapped;
     }
-    if (e == hipSuccess) {
+    if (e == hipSuccess && n > m0) {
         hipMemAccessDesc acc = {};
         acc.location = prop.location;
         acc.flags = hipMemAccessFlagsProtReadWrite;
-        e = hipMemSetAccess(ptr, b->bytes, &acc, 1);
+        e = hipMemSetAccess(static_cast<char*>(ptr) + m0 * b->chunk, (n - m0) * b->chunk, &acc, 1);
     }
-    if (e != hipSuccess) {
-        // never mapped for a kernel (hipMemSetAccess is the last step), so the range may go back as well
-        for (size_t i = 0; i < mapped; ++i) (void)hipMemUnmap(static_cast<char*>(ptr) + i * chunk, chunk);
-        for (auto& c : b->chunks) (void)hipMemRelease(c);
-        b->chunks.clear();
-        (void)hipMemAddressFree(ptr, b->bytes);
+    if (e != hipSuccess) {   // chunks mapped by this call were never accessed by a kernel: undo them
+        for (size_t i = m0; i < b->chunks.size(); ++i) {
+            (void)hipMemUnmap(static_cast<char*>(ptr) + i * b->chunk, b->chunk);
+            (void)hipMemRelease(b->chunks[i]);
+        }
+        b->chunks.resize(m0);
+    }
+    return e;
+}
+
+// Reserve a class-sized range and map its first n chunks.
+hipError_t hbm_create(int device, size_t n, size_t chunk, const hipMemAllocationProp& prop, void** out, HbmBuffer* b) {
+    b->device = device;
+    b->chunk = chunk;
+    b->cls = hbm_class(n);
+    void* ptr = nullptr;
+    hipError_t e = hipMemAddressReserve(&ptr, b->reserved_bytes(), chunk, nullptr, 0);
+    if (e != hipSuccess) return e;
+    b->chunks.reserve(n);
+    e = hbm_map_to(ptr, b, n, prop);
+    if (e != hipSuccess) {                               // never mapped for a kernel: the range may go back
+        (void)hipMemAddressFree(ptr, b->reserved_bytes());
         return e;
     }
     *out = ptr;
@@ -1062,36 +1141,67 @@ sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out) {
     HIP_TRY(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
     if (gran == 0) gran = 4096;
     const size_t chunk = (hbm_chunk_bytes() + gran - 1) / gran * gran;
-    const size_t n = (size_t)((bytes + chunk - 1) / chunk);
-    std::lock_guard<std::mutex> lk(g_hbm_mu);
-    HIP_TRY(hbm_trim_locked(device, hbm_pool_cap()));
-    {   // a pooled buffer of this device that fits, the smallest one (at most twice the size)
+    const size_t n = (size_t)((bytes + chunk - 1) / chunk), cls = hbm_class(n);
+    // 1. a pooled buffer of this class (the one with the most chunks mapped up to n; fewest past n): taken out
+    //    of the pool under the lock, waited for and grown outside it
+    uintptr_t key = 0;
+    HbmBuffer b;
+    bool need_sync = false;
+    {
+        std::lock_guard<std::mutex> lk(g_hbm_mu);
         auto best = g_hbm_pool.end();
+        auto rank = [&](const HbmBuffer& c) { return c.chunks.size() >= n ? c.chunks.size() - n : 4 * (n - c.chunks.size()); };
         for (auto it = g_hbm_pool.begin(); it != g_hbm_pool.end(); ++it) {
             const HbmBuffer& c = it->second;
-            if (c.device == device && c.bytes >= bytes && c.bytes <= 2 * n * chunk &&
-                (best == g_hbm_pool.end() || c.bytes < best->second.bytes))
+            if (c.device == device && c.chunk == chunk && c.cls == cls &&
+                (best == g_hbm_pool.end() || rank(c) < rank(best->second)))
                 best = it;
         }
         if (best != g_hbm_pool.end()) {
-            if (best->second.freed_epoch == g_hbm_epoch[device]) {   // freed since the last sync: may be in use
-                HIP_TRY(hipDeviceSynchronize());
-                ++g_hbm_epoch[device];
-            }
-            *out = reinterpret_cast<void*>(best->first);
-            g_hbm[best->first] = std::move(best->second);
+            key = best->first;
+            b = std::move(best->second);
             g_hbm_pool.erase(best);
-            return ok();
+            need_sync = !hbm_idle(b);
         }
     }
-    HbmBuffer b;
+    if (key) {
+        hipError_t e = need_sync ? hbm_sync(device) : hipSuccess;
+        if (e == hipSuccess && b.chunks.size() < n) {
+            e = hbm_map_to(reinterpret_cast<void*>(key), &b, n, prop);
+            if (e == hipErrorOutOfMemory) {              // give the rest of the pool back, then retry once
+                (void)hipGetLastError();
+                (void)hbm_trim(device, 0);
+                e = hbm_map_to(reinterpret_cast<void*>(key), &b, n, prop);
+            }
+        }
+        std::lock_guard<std::mutex> lk(g_hbm_mu);
+        if (e != hipSuccess) {                           // back to the pool as it was
+            g_hbm_pool[key] = std::move(b);
+            (void)hipGetLastError();
+            return fail(e == hipErrorOutOfMemory ? SDA_ERR_OUT_OF_MEMORY : SDA_ERR_DEVICE,
+                        "sda_hbm_alloc(%llu bytes): growing a pooled buffer: %s", (unsigned long long)bytes,
+                        hipGetErrorString(e));
+        }
+        g_hbm[key] = std::move(b);
+        *out = reinterpret_cast<void*>(key);
+        return ok();
+    }
+    // 2. a new buffer: the pool first goes down to its bound
+    HIP_TRY(hbm_trim(device, hbm_pool_cap()));
     void* ptr = nullptr;
     hipError_t e = hbm_create(device, n, chunk, prop, &ptr, &b);
-    if (e == hipErrorOutOfMemory && hbm_pooled_bytes(device) > 0) {   // give the pool back, then retry once
-        (void)hipGetLastError();
-        HIP_TRY(hbm_trim_locked(device, 0));
-        b = HbmBuffer();
-        e = hbm_create(device, n, chunk, prop, &ptr, &b);
+    if (e == hipErrorOutOfMemory) {                      // give the pool back, then retry once
+        bool any;
+        {
+            std::lock_guard<std::mutex> lk(g_hbm_mu);
+            any = hbm_pooled_bytes(device) > 0;
+        }
+        if (any) {
+            (void)hipGetLastError();
+            HIP_TRY(hbm_trim(device, 0));
+            b = HbmBuffer();
+            e = hbm_create(device, n, chunk, prop, &ptr, &b);
+        }
     }
     if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -1099,6 +1209,7 @@ sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out) {
                     "sda_hbm_alloc(%llu bytes in %zu MiB chunks): %s", (unsigned long long)bytes, chunk >> 20,
                     hipGetErrorString(e));
     }
+    std::lock_guard<std::mutex> lk(g_hbm_mu);
     g_hbm[reinterpret_cast<uintptr_t>(ptr)] = std::move(b);
     *out = ptr;
     return ok();
@@ -1107,22 +1218,27 @@ sda_status sda_hbm_alloc(int device, uint64_t bytes, void** out) {
 sda_status sda_hbm_free(void* ptr) {
     SDA_ENTRY;
     if (!ptr) return ok();
-    std::lock_guard<std::mutex> lk(g_hbm_mu);
-    auto it = g_hbm.find(reinterpret_cast<uintptr_t>(ptr));
-    if (it == g_hbm.end()) return fail(SDA_ERR_INVALID_ARGUMENT, "%p was not returned by sda_hbm_alloc (or freed twice)", ptr);
-    if (hbm_pool_cap() == 0) {   // no pool (SDA_HBM_POOL_MB=0): release at once, after the device is idle
-        DeviceGuard dg;
-        HIP_TRY(hipSetDevice(it->second.device));
-        HIP_TRY(hipDeviceSynchronize());
-        ++g_hbm_epoch[it->second.device];
-        hbm_release(ptr, it->second, it->second.chunks.size());
+    HbmBuffer b;
+    {
+        std::lock_guard<std::mutex> lk(g_hbm_mu);
+        auto it = g_hbm.find(reinterpret_cast<uintptr_t>(ptr));
+        if (it == g_hbm.end())
+            return fail(SDA_ERR_INVALID_ARGUMENT, "%p was not returned by sda_hbm_alloc (or freed twice)", ptr);
+        if (hbm_pool_cap() != 0) {                       // pooled: no wait
+            it->second.freed_ticket = g_hbm_sync_begun[it->second.device];
+            it->second.freed_seq = ++g_hbm_seq;
+            g_hbm_pool[it->first] = std::move(it->second);
+            g_hbm.erase(it);
+            return ok();
+        }
+        b = std::move(it->second);
         g_hbm.erase(it);
-        return ok();
     }
-    it->second.freed_epoch = g_hbm_epoch[it->second.device];
-    it->second.freed_seq = ++g_hbm_seq;
-    g_hbm_pool[it->first] = std::move(it->second);
-    g_hbm.erase(it);
+    // no pool (SDA_HBM_POOL_MB=0): release at once, after the device is idle
+    DeviceGuard dg;
+    HIP_TRY(hipSetDevice(b.device));
+    HIP_TRY(hbm_sync(b.device));
+    hbm_release(ptr, b);
     return ok();
 }
 
@@ -1131,8 +1247,7 @@ sda_status sda_hbm_trim(int device, uint64_t keep_bytes) {
     if (device < 0 || device >= kHbmMaxDev) return fail(SDA_ERR_INVALID_ARGUMENT, "device %d out of range", device);
     DeviceGuard dg;
     HIP_TRY(hipSetDevice(device));
-    std::lock_guard<std::mutex> lk(g_hbm_mu);
-    HIP_TRY(hbm_trim_locked(device, keep_bytes));
+    HIP_TRY(hbm_trim(device, keep_bytes));
     return ok();
 }
 
@@ -1142,7 +1257,7 @@ sda_status sda_hbm_stats(int device, uint64_t* live_bytes, uint64_t* pooled_byte
     std::lock_guard<std::mutex> lk(g_hbm_mu);
     uint64_t live = 0;
     for (auto& kv : g_hbm)
-        if (kv.second.device == device) live += kv.second.bytes;
+        if (kv.second.device == device) live += kv.second.mapped_bytes();
     if (live_bytes) *live_bytes = live;
     if (pooled_bytes) *pooled_bytes = hbm_pooled_bytes(device);
     if (retired_bytes) *retired_bytes = g_hbm_retired[device];

@@ -90,6 +90,33 @@ RAND03_SEED_0_7_STRIDE17 = [
     0x11cfa18e, 0xd3c50049, 0x75c775f6, 0x434c6530, 0x2c5bad8f, 0x898881dc, 0x5f1c86d9, 0xc1f8e7f4]
 
 
+def checksum(words: np.ndarray):
+    """sum_i w_i k_i and sum_i (w_i ^ k_i) mod 2^64, k_i = splitmix64_at(0xC5C5, i) | 1 (tests/abi_c/hbm_cycle.c)."""
+    from sda_amd.synth import splitmix64_at
+    w = np.ascontiguousarray(words, np.int64).reshape(-1).view(np.uint64)
+    k = splitmix64_at(0xC5C5, np.arange(w.size, dtype=np.uint64)) | np.uint64(1)
+    with np.errstate(over="ignore"):
+        return int(np.sum(w * k, dtype=np.uint64)), int(np.sum(w ^ k, dtype=np.uint64))
+
+
+def abi_c_sharegen():
+    from sda_amd import synth
+    sch = S.CONFIG_PACKED
+    p, k, t, n, D = sch.prime_modulus, sch.secret_count, sch.privacy_threshold(), sch.share_count, 1_000_000
+    B = D // k
+    secrets = synth.fill(1, D, 0x5DA + 2, 0, p).reshape(-1)
+    draws = synth.fill(B, t, 0x5DA + 3, 0, p - 1).reshape(-1)
+    pp = O.packed_params(k, n, t, p, sch.omega_secrets, sch.omega_shares)
+    shares = O.packed_generate(pp, secrets, draws)
+    # the shares reveal to the secrets (a property check of the fixture itself)
+    rc, rec = O.packed_reconstruct(pp, 4 * k, list(range(k + t)), shares[:k + t, :4])
+    assert rc == 0 and (np.mod(rec, p) == secrets[:4 * k]).all()
+    c1, c2 = checksum(shares)
+    return {"scheme": scheme_json(sch), "dimension": D, "secret_seed": 0x5DA + 2, "draw_seed": 0x5DA + 3,
+            "layout": "[n][B] clerk-major, i64", "checksum": [c1, c2],
+            "secrets_checksum": list(checksum(secrets)), "draws_checksum": list(checksum(draws))}
+
+
 def main():
     be = OracleBackend()
     out = {}
@@ -182,6 +209,10 @@ def main():
         packed.append({"scheme": scheme_json(sch), "secrets": secrets.tolist(), "draws": draws.tolist(),
                        "shares": shares.tolist(), "reveals": reveals})
     out["packed_cases.json"] = packed
+
+    # 7. configs[2] at 1M-dim for the torch-free C consumer (tests/abi_c/hbm_cycle.c `gen`): the inputs of
+    #    sda_synth_fill_dev (seeds 0x5DA + 2 / + 3), the oracle's tss shares, two order-sensitive checksums
+    out["abi_c_sharegen.json"] = abi_c_sharegen()
 
     for name, obj in out.items():
         with open(os.path.join(HERE, name), "w") as f:

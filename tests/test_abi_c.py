@@ -58,9 +58,20 @@ def _parse(out):
     return res
 
 
+HBM_BIN = os.path.join(HERE, "abi_c", "hbm_cycle")
+
+
 def _ensure_built():
-    if not os.path.exists(BIN):
+    if not (os.path.exists(BIN) and os.path.exists(HBM_BIN)):
         subprocess.run(["make", "-C", os.path.dirname(BIN)], check=True, capture_output=True)
+
+
+def _hbm_cycle(*args, timeout=300):
+    _ensure_built()
+    env = {k: val for k, val in os.environ.items() if not k.startswith(("PYTHON", "SDA_HBM"))}
+    r = subprocess.run([HBM_BIN, *args], capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, (r.stdout, r.stderr)
+    return {k.strip(): v.split() for k, v in (l.split(":", 1) for l in r.stdout.splitlines() if ":" in l)}
 
 
 @pytest.mark.parametrize("devices", ["", "0", "0,0,0"], ids=["handle", "multi1", "multi3"])
@@ -95,3 +106,32 @@ def test_c_program_does_not_load_torch():
     _ensure_built()
     r = subprocess.run(["ldd", BIN], capture_output=True, text=True, timeout=60)
     assert "libsda_engine.so" in r.stdout and "/opt/rocm" in r.stdout and "torch" not in r.stdout
+
+
+def test_c_hbm_trim_realloc_sequence():
+    """The round-4 corruption's sequence (tests/test_gpu_hbm.py::test_hbm_trim_realloc_sequence_matches_torch) on
+    the ROCm runtime the Rust shim would load: three rounds of a filled 2.4 GB buffer freed and released, a
+    foreign hipMalloc block, new sda_hbm buffers (none in a retired range) and share-gen into one of them, equal
+    to share-gen into a hipMalloc buffer on two reads, the foreign block untouched (tests/abi_c/hbm_cycle.c)."""
+    out = _hbm_cycle("seq")
+    assert out["seq"][0] == "ok" and int(out["seq"][4]) == 0          # pooled 0 after the final trim
+    assert int(out["seq"][6]) > 0                                       # the released ranges were retired
+
+
+def test_c_configs2_share_gen_matches_fixture():
+    """configs[2] (k=8 n=26 t=7, p = 2147482801) at 1M-dim from plain C: the host entry point and the _dev entry
+    point into an sda_hbm buffer both give the oracle's tss shares (checksums, tests/golden/abi_c_sharegen.json)."""
+    with open(os.path.join(HERE, "golden", "abi_c_sharegen.json")) as f:
+        want = [str(x) for x in json.load(f)["checksum"]]
+    out = _hbm_cycle("gen")
+    assert out["gen_host"] == want and out["gen_dev"] == want
+
+
+def test_c_hbm_10000_mixed_cycles_retire_nothing():
+    """10,000 jobs of 1-3 buffers of 2-192 MiB (2 MiB chunks): size-class reuse keeps the pool bounded and no
+    trim happens, so not one byte of address space is retired (the bound this test states: 0 bytes with the
+    default SDA_HBM_POOL_MB; the pool's peak stays far below it)."""
+    out = _hbm_cycle("cycle", "10000", timeout=600)
+    c = dict(zip(out["cycle"][0::2], (int(x) for x in out["cycle"][1::2])))
+    assert c["cycles"] == 10000 and c["retired"] == 0 and c["live"] == 0
+    assert c["peak_pooled"] < (32768 << 20) // 4

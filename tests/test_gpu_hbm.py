@@ -126,25 +126,61 @@ def test_hbm_trim_realloc_sequence_matches_torch(engine, monkeypatch):
 
 
 def test_hbm_pool_is_bounded(engine, monkeypatch):
-    """Freed buffers beyond SDA_HBM_POOL_MB are trimmed (oldest first) at the next allocation; a pooled buffer
-    is handed out again while it fits the bound; sda_hbm_trim empties the pool."""
-    import torch
+    """Freed buffers only pool (no wait, no trim).  A request of the same size class takes a pooled buffer back
+    without trimming anything; one that needs a new buffer first trims the pool (oldest first) to
+    SDA_HBM_POOL_MB; sda_hbm_trim empties the pool."""
     engine.hbm_trim(0)
     monkeypatch.setenv("SDA_HBM_POOL_MB", "256")
-    bufs = [engine.hbm_empty((16 << 20,)) for _ in range(4)]    # 4 x 128 MiB
+    bufs = [engine.hbm_empty((16 << 20,)) for _ in range(4)]    # 4 x 128 MiB (2 chunks, class 2)
     ptrs = [b.data_ptr() for b in bufs]
     for i in range(4):                                         # freed in order: bufs[0] is the oldest
         bufs[i] = None
-    live, pooled, _ = engine.hbm_stats()
+    live, pooled, retired0 = engine.hbm_stats()
     assert pooled >= 4 * (128 << 20)                           # free only pools (no wait, no trim)
-    x = engine.hbm_empty((16 << 20,))                          # trims to 256 MiB, then reuses a pooled buffer
-    assert x.data_ptr() in ptrs[2:]                            # the two oldest were trimmed
-    live, pooled, _ = engine.hbm_stats()
-    assert pooled <= 256 << 20
+    x = engine.hbm_empty((16 << 20,))                          # same class: a pooled buffer, nothing trimmed
+    assert x.data_ptr() in ptrs
+    assert engine.hbm_stats()[1] == 3 * (128 << 20) and engine.hbm_stats()[2] == retired0
+    y = engine.hbm_empty((48 << 20,))                          # 384 MiB, class 6: new, after a trim to 256 MiB
+    live, pooled, retired = engine.hbm_stats()
+    assert pooled <= 256 << 20 and retired == retired0 + (128 << 20)
+    assert y.data_ptr() not in ptrs
     x.fill_(7)
-    assert int(x.sum()) == 7 * x.numel()
-    del x
+    y.fill_(-3)
+    assert int(x.sum()) == 7 * x.numel() and int(y.sum()) == -3 * y.numel()
+    del x, y
     engine.hbm_trim(0)
     assert engine.hbm_stats()[1] == 0
     with pytest.raises(SdaError):
         E._check(engine.lib.sda_hbm_trim(-1, 0))
+
+
+def test_hbm_size_class_grows_a_pooled_buffer(engine):
+    """A pooled buffer serves a larger request of its size class by mapping fresh chunks at its reserved
+    range's never-mapped tail: same pointer, more bytes live, the new tail usable by torch and the engine."""
+    import torch
+    engine.hbm_trim(0)
+    chunk = 8 << 20                                            # int64 elements per 64 MiB chunk
+    live0 = engine.hbm_stats()[0]
+    a = engine.hbm_empty((9 * chunk,))                         # 9 chunks: class 10 (9 mapped)
+    pa = a.data_ptr()
+    a.fill_(1)
+    del a
+    b = engine.hbm_empty((9 * chunk - 1000,))                  # same class, fewer bytes: handed back as is
+    assert b.data_ptr() == pa and engine.hbm_stats()[0] - live0 == 9 * (64 << 20)
+    del b
+    c = engine.hbm_empty((11 * chunk,))                        # class 12: a new buffer
+    assert c.data_ptr() != pa
+    del c
+    d = engine.hbm_empty((10 * chunk,))                        # 10 chunks, class 10: the pooled one, grown
+    assert d.data_ptr() == pa
+    live, _, _ = engine.hbm_stats()
+    assert live - live0 == 10 * (64 << 20)
+    st = torch.cuda.current_stream().cuda_stream
+    engine.synth_fill_dev(d.data_ptr(), 1, d.numel(), 5, -9, 9, st)
+    ref = torch.empty_like(d)
+    engine.synth_fill_dev(ref.data_ptr(), 1, d.numel(), 5, -9, 9, st)
+    assert torch.equal(d, ref)
+    d.fill_(4)
+    assert int(d[-chunk:].sum()) == 4 * chunk                  # the grown tail
+    del d
+    engine.hbm_trim(0)
