@@ -23,6 +23,8 @@ cp "$S/bench_11.json" "$D/configs/config4.json"
 cp "$S/bench_11.log" "$D/configs/config4.log"
 cp "$S/pmc_12.txt" "$D/pmc_c3_fetch.txt" 2>/dev/null || true
 cp "$S/pmc_13.txt" "$D/pmc_c3_write.txt" 2>/dev/null || true
+cp "$S/pmc_14.txt" "$D/pmc_codec_fetch.txt" 2>/dev/null || true
+cp "$S/pmc_15.txt" "$D/pmc_codec_write.txt" 2>/dev/null || true
 python3 - "$TAG" <<'EOF'
 import json, re, sys
 tag = sys.argv[1]

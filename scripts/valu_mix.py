@@ -27,8 +27,8 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-o
 
 # (bench key, source, -D define or None, mangled-name fragment)
 KERNELS = [
-    ("gen_exact", "packed_gen.hip", "SDA_GEN_PART=27", "packed_gen_kernelILi16ELi27ELb1ELb0ELb1ELb1E"),
-    ("gen_canonical", "packed_gen.hip", "SDA_GEN_PART=27", "packed_gen_kernelILi16ELi27ELb1ELb1ELb0ELb0E"),
+    ("gen_exact", "packed_gen.hip", "SDA_GEN_PART=27 -DSDA_GEN_L=16", "packed_gen_kernelILi16ELi27ELb1ELb0ELb1ELb1E"),
+    ("gen_canonical", "packed_gen.hip", "SDA_GEN_PART=27 -DSDA_GEN_L=16", "packed_gen_kernelILi16ELi27ELb1ELb1ELb0ELb0E"),
     ("reveal_exact", "packed_reveal.hip", "SDA_REVEAL_PART=16", "packed_reveal_exact_kernelILi16ELb1ELi8ELb1ELb1E"),
     ("reveal_canonical", "packed_reveal.hip", "SDA_REVEAL_PART=16", "packed_reveal_canon_kernelILi16ELb1E"),
     ("chacha_combine", "chacha.hip", None, "chacha_combine_sk_kernelILb1ELb1E"),
@@ -95,7 +95,7 @@ def rate_of(op, R):
 def disasm(src, define, frag):
     with tempfile.TemporaryDirectory() as d:
         obj = os.path.join(d, "k.o")
-        cmd = [HIPCC] + FLAGS + ([f"-D{define}"] if define else []) + ["-c", os.path.join(ROOT, "sda_amd", "csrc", src),
+        cmd = [HIPCC] + FLAGS + ([f"-D{x}" for x in define.split(" -D")] if define else []) + ["-c", os.path.join(ROOT, "sda_amd", "csrc", src),
                                                                        "-o", obj]
         subprocess.run(cmd, check=True, capture_output=True)
         txt = subprocess.run([OBJDUMP, "-d", obj], check=True, capture_output=True, text=True).stdout
