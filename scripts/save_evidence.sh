@@ -31,13 +31,14 @@ tag = sys.argv[1]
 def kib(path, ctr, acc="false"):
     # acc: the accumulating instantiation (configs[3]'s row tiles) is <long, 2, 8, true, true, false>
     txt = open(f"profiles/{tag}/{path}").read()
-    m = re.search(r"combine_exact_kernel<long, 2, 8, true, " + acc + r", false>\n\s+" + ctr + r"\s+([0-9.e+]+)", txt)
+    # the pipelined kernel since round 6: <long, 2, 4, SMALL_M, ACC, FLAG, PIPE>
+    m = re.search(r"combine_exact_kernel<long, 2, 4, true, " + acc + r", false, true>\n\s+" + ctr + r"\s+([0-9.e+]+)", txt)
     return float(m.group(1))
 import csv
 def trace_avg_ms(grid_x):
     # the dominant combine launch's average in this session's rocprofv3 --kernel-trace (kernel_stats_by_grid.csv)
     for r in csv.DictReader(open(f"profiles/{tag}/kernel_stats_by_grid.csv")):
-        if r["kernel"].startswith("sda::combine_exact_kernel<long, 2, 8, true, false, false>") and \
+        if r["kernel"].startswith("sda::combine_exact_kernel<long, 2, 4, true, false, false, true>") and \
                 int(r["grid_x"]) == grid_x:
             return float(r["avg_us"]) / 1e3, int(r["calls"])
     return None, 0

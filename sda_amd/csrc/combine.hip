@@ -8,7 +8,9 @@
 // is still read exactly once with fully coalesced loads (a wave reads 64 * VEC * 8 contiguous
 // bytes of one row per instruction).  UNROLL rows are loaded before the dependent chain so
 // every lane keeps UNROLL * VEC * 8 bytes in flight; with ~30 waves per CU that covers HBM
-// latency.  Non-temporal loads keep the once-read stream from thrashing L2/MALL.
+// latency.  The i64 kernels are software-pipelined (PIPE: the next 4 rows load while the current 4
+// rows' chain runs), so a wave never sits computing with nothing in flight.  Non-temporal loads keep
+// the once-read stream from thrashing L2/MALL.
 //
 // Roofline: HBM.  Algorithmic bytes per launch = 8 * n * dim (read) + 8 * dim (write)
 // (4 * n * dim read for the int32 rows of the clerk's decode -> combine).
@@ -37,7 +39,10 @@ __device__ __forceinline__ int64_t lane_of(const typename vec_t<T, VEC>::type& v
 // runs its replay pass) and flags[1] when an input lies outside [-(2^63 - m), 2^63 - m] (the
 // reference's `r + v` may wrap i64 there, which no split can reproduce).  One OR of the high word per
 // element (plus a 64-bit range check); every writer stores the same 1, so plain stores suffice.
-template <typename T, int VEC, int UNROLL, bool SMALL_M, bool ACC, bool FLAG = false>
+// PIPE (the i64 default since round 6; SDA_COMBINE_PIPE=0 turns it off): software-pipelined -- the next UNROLL
+// rows are loaded before the current UNROLL rows' dependent chain runs, so a wave keeps loads in flight while it
+// computes (two register buffers).
+template <typename T, int VEC, int UNROLL, bool SMALL_M, bool ACC, bool FLAG = false, bool PIPE = false>
 __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict__ in,
                                                             uint64_t n, uint64_t n_lanes,
                                                             uint64_t stride,
@@ -63,15 +68,46 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict_
         }
     };
     uint64_t i = 0;
-    for (; i + UNROLL <= n; i += UNROLL) {
-        V v[UNROLL];
+    if constexpr (PIPE) {
+        // every load is unconditional (a batch past the last whole one re-reads the last whole batch): a load on
+        // one side of a branch makes the compiler's counter merge wait for it before the other buffer's use
+        const uint64_t full = n - n % UNROLL;           // rows in whole batches (uniform)
+        const V* p0 = p;
+        V a[UNROLL], b[UNROLL];
+        auto load = [&](V (&x)[UNROLL], uint64_t r0) {
+            const uint64_t rc = r0 < full ? r0 : full - UNROLL;
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) v[u] = __builtin_nontemporal_load(p + (uint64_t)u * vstride);
-        p += (uint64_t)UNROLL * vstride;
+            for (int u = 0; u < UNROLL; ++u) x[u] = __builtin_nontemporal_load(p0 + (rc + u) * vstride);
+        };
+        auto chain = [&](const V (&x)[UNROLL]) {
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u)
+            for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) step(e, lane_of<T, VEC>(v[u], e));
+                for (int e = 0; e < VEC; ++e) step(e, lane_of<T, VEC>(x[u], e));
+        };
+        if (full) {
+            load(a, 0);
+            for (uint64_t j = 0; j < full; j += 2 * UNROLL) {
+                load(b, j + UNROLL);
+                chain(a);
+                if (j + UNROLL >= full) break;
+                load(a, j + 2 * UNROLL);
+                chain(b);
+            }
+        }
+        i = full;
+        p = p0 + full * vstride;
+    } else {
+        for (; i + UNROLL <= n; i += UNROLL) {
+            V v[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) v[u] = __builtin_nontemporal_load(p + (uint64_t)u * vstride);
+            p += (uint64_t)UNROLL * vstride;
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+                for (int e = 0; e < VEC; ++e) step(e, lane_of<T, VEC>(v[u], e));
+        }
     }
     for (; i < n; ++i) {
         V v = __builtin_nontemporal_load(p);
@@ -92,18 +128,27 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict_
     reinterpret_cast<VO*>(out)[lane] = o;
 }
 
-template <typename T, int VEC, int UNROLL, bool ACC, bool FLAG = false>
+template <typename T, int VEC, int UNROLL, bool ACC, bool FLAG = false, bool PIPE = false>
 hipError_t launch_vec(const T* in, uint64_t n, uint64_t dim, uint64_t stride, int64_t* out,
                       const Mod64& M, bool small_m, hipStream_t s, int64_t* flags = nullptr) {
     const uint64_t n_lanes = dim / VEC;
     const uint64_t blocks = (n_lanes + 255) / 256;
     if (small_m)
-        hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, true, ACC, FLAG>), dim3((unsigned)blocks), dim3(256),
-                           0, s, in, n, n_lanes, stride, out, M, flags);
+        hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, true, ACC, FLAG, PIPE>), dim3((unsigned)blocks),
+                           dim3(256), 0, s, in, n, n_lanes, stride, out, M, flags);
     else
-        hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, false, ACC, FLAG>), dim3((unsigned)blocks), dim3(256),
-                           0, s, in, n, n_lanes, stride, out, M, flags);
+        hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, false, ACC, FLAG, PIPE>), dim3((unsigned)blocks),
+                           dim3(256), 0, s, in, n, n_lanes, stride, out, M, flags);
     return hipGetLastError();
+}
+
+// The i64 kernels run software-pipelined, two buffers of 4 rows (PIPE): one process, one 80 GB buffer, the
+// variants interleaved (scripts/combine_pipe_inproc.py, profiles/r06m): 12.298 ms unpipelined (8 rows per
+// batch), 12.134 ms pipelined at 4 rows, 12.175 at 6, 12.192 at 2; bit-identical.  SDA_COMBINE_PIPE=0 (A/B
+// knob) launches the unpipelined kernel.
+bool combine_pipe() {
+    const char* e = getenv("SDA_COMBINE_PIPE");
+    return !(e && e[0] == '0');
 }
 
 // canonical residue in [0, m) of a signed i64 value
@@ -234,9 +279,13 @@ hipError_t launch_combine_exact(const int64_t* in, uint64_t n, uint64_t dim, uin
     const uintptr_t a = (uintptr_t)in | (uintptr_t)out;
     // widest vector whose columns, row stride and base addresses all line up
     const bool v2 = dim % 2 == 0 && stride % 2 == 0 && (a % 16) == 0;
-    if (accumulate)
+    const bool pipe = v2 && combine_pipe();
+    if (accumulate) {
+        if (pipe) return launch_vec<int64_t, 2, 4, true, false, true>(in, n, dim, stride, out, M, small_m, s);
         return v2 ? launch_vec<int64_t, 2, 8, true>(in, n, dim, stride, out, M, small_m, s)
                   : launch_vec<int64_t, 1, 8, true>(in, n, dim, stride, out, M, small_m, s);
+    }
+    if (pipe) return launch_vec<int64_t, 2, 4, false, false, true>(in, n, dim, stride, out, M, small_m, s);
     return v2 ? launch_vec<int64_t, 2, 8, false>(in, n, dim, stride, out, M, small_m, s)
               : launch_vec<int64_t, 1, 8, false>(in, n, dim, stride, out, M, small_m, s);
 }
@@ -248,6 +297,8 @@ hipError_t launch_combine_split(const int64_t* in, uint64_t n, uint64_t dim, uin
     const bool small_m = modulus <= ((int64_t)1 << 62);
     const uintptr_t a = (uintptr_t)in | (uintptr_t)inout;
     const bool v2 = dim % 2 == 0 && stride % 2 == 0 && (a % 16) == 0;
+    if (v2 && combine_pipe())
+        return launch_vec<int64_t, 2, 4, true, true, true>(in, n, dim, stride, inout, M, small_m, s, flags);
     return v2 ? launch_vec<int64_t, 2, 8, true, true>(in, n, dim, stride, inout, M, small_m, s, flags)
               : launch_vec<int64_t, 1, 8, true, true>(in, n, dim, stride, inout, M, small_m, s, flags);
 }
