@@ -3,6 +3,7 @@ round 6's tuning the knob also took the depths 2 / 4 / 6 / 8, profiles/r06m): on
 10k x 1M i64 buffer, the variants interleaved launch block by launch block, HIP events on the launch stream, so
 buffer placement and box state are shared by every variant.  Also checks the variants agree bit for bit.
     python scripts/combine_pipe_inproc.py [rounds] [variants ...]
+SDA_INPROC_SHAPE=acc times the accumulating kernel on configs[3]'s 1000 x 10M tile instead.
 """
 import os
 import sys
@@ -17,20 +18,30 @@ rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 variants = sys.argv[2:] or ["0", "1"]
 torch.cuda.init()
 eng = Engine(0)
-N, D = 10_000, 1_000_000
+acc = os.environ.get("SDA_INPROC_SHAPE") == "acc"
+N, D = (1_000, 10_000_000) if acc else (10_000, 1_000_000)
 x = torch.empty((N, D), dtype=torch.int64, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 eng.synth_fill_dev(x.data_ptr(), N, D, 0x5DB, -(M - 1), M, st)      # signed: the order-dependent worst case
-outs = {v: torch.empty(D, dtype=torch.int64, device="cuda") for v in variants}
+outs = {v: torch.zeros(D, dtype=torch.int64, device="cuda") for v in variants}
+
+
+def launch(v):
+    if acc:
+        eng.combine_accumulate_dev(M, x.data_ptr(), N, D, D, outs[v].data_ptr(), st)
+    else:
+        eng.combine_dev(M, x.data_ptr(), N, D, D, outs[v].data_ptr(), st)
+
+
 res = {v: [] for v in variants}
 for r in range(rounds):
     for v in variants:
         os.environ["SDA_COMBINE_PIPE"] = v
-        eng.combine_dev(M, x.data_ptr(), N, D, D, outs[v].data_ptr(), st)          # warm
+        launch(v)                                                                   # warm
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(10):
-            eng.combine_dev(M, x.data_ptr(), N, D, D, outs[v].data_ptr(), st)
+            launch(v)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 10

@@ -69,15 +69,15 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict_
     };
     uint64_t i = 0;
     if constexpr (PIPE) {
-        // every load is unconditional (a batch past the last whole one re-reads the last whole batch): a load on
-        // one side of a branch makes the compiler's counter merge wait for it before the other buffer's use
+        // a buffer's loads are issued on every path that reaches its chain, and the last whole batch is peeled
+        // off: a load on one side of a branch makes the compiler's counter merge wait for it before the other
+        // buffer's use
         const uint64_t full = n - n % UNROLL;           // rows in whole batches (uniform)
         const V* p0 = p;
         V a[UNROLL], b[UNROLL];
         auto load = [&](V (&x)[UNROLL], uint64_t r0) {
-            const uint64_t rc = r0 < full ? r0 : full - UNROLL;
 #pragma unroll
-            for (int u = 0; u < UNROLL; ++u) x[u] = __builtin_nontemporal_load(p0 + (rc + u) * vstride);
+            for (int u = 0; u < UNROLL; ++u) x[u] = __builtin_nontemporal_load(p0 + (r0 + u) * vstride);
         };
         auto chain = [&](const V (&x)[UNROLL]) {
 #pragma unroll
@@ -87,10 +87,11 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict_
         };
         if (full) {
             load(a, 0);
-            for (uint64_t j = 0; j < full; j += 2 * UNROLL) {
+            for (uint64_t j = 0;; j += 2 * UNROLL) {        // a holds rows j.., in flight
+                if (j + UNROLL == full) { chain(a); break; }
                 load(b, j + UNROLL);
                 chain(a);
-                if (j + UNROLL >= full) break;
+                if (j + 2 * UNROLL == full) { chain(b); break; }
                 load(a, j + 2 * UNROLL);
                 chain(b);
             }
