@@ -167,10 +167,12 @@ def test_packed_generate_fixup_overflow(engine, oracle):
         assert_same(shares[:, b], exp)
 
 
-def test_combine_accumulate_tiles(engine, oracle):
-    """sda_combine_accumulate_dev: a job streamed in row tiles == one pass (signed, order-dependent)."""
+@pytest.mark.parametrize("D", [3001, 3000], ids=["odd_dim", "even_dim_pipelined"])
+def test_combine_accumulate_tiles(engine, oracle, D):
+    """sda_combine_accumulate_dev: a job streamed in row tiles == one pass (signed, order-dependent); an even
+    dimension runs the software-pipelined kernel (2 columns per lane), an odd one the 1-column kernel."""
     m = 2147482801
-    N, D = 37, 3001
+    N = 37
     x = np.random.default_rng(9).integers(-(m - 1), m, size=(N, D), dtype=np.int64)
     xd = torch.as_tensor(x).cuda()
     acc = torch.zeros(D, dtype=torch.int64, device="cuda")
@@ -317,3 +319,25 @@ def test_finalize_signed_sums(engine):
     engine.combine_finalize_dev(m, s.data_ptr(), s.numel(), out.data_ptr(), _stream())
     torch.cuda.synchronize()
     assert out.tolist() == [int(v) % m for v in s.tolist()]
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"], ids=["pipelined", "unpipelined"])
+def test_combine_pipelined_row_counts(engine, oracle, monkeypatch, pipe):
+    """combine.hip's software-pipelined i64 kernel (two buffers of 4 rows, the last whole batch peeled off) at
+    every row count from 1 to 21 -- no whole batch, an odd and an even number of them, each with 0-3 tail rows --
+    plain and accumulating, signed inputs (the order-dependent case), against the reference recurrence."""
+    monkeypatch.setenv("SDA_COMBINE_PIPE", pipe)
+    m, D = 2147482801, 2 * 1543
+    rng = np.random.default_rng(1543)
+    x = rng.integers(-(m - 1), m, size=(21, D), dtype=np.int64)
+    xd = torch.as_tensor(x).cuda()
+    for N in range(1, 22):
+        out = torch.empty(D, dtype=torch.int64, device="cuda")
+        engine.combine_dev(m, xd.data_ptr(), N, D, D, out.data_ptr(), _stream())
+        torch.cuda.synchronize()
+        assert_same(out.cpu().numpy(), oracle.combine(m, x[:N]), f"N={N}")
+    for N in range(1, 21):
+        acc = torch.as_tensor(x[0]).cuda()                   # the state after row 0; then rows 1..N
+        engine.combine_accumulate_dev(m, xd[1].data_ptr(), N, D, D, acc.data_ptr(), _stream())
+        torch.cuda.synchronize()
+        assert_same(acc.cpu().numpy(), oracle.combine(m, x[:N + 1]), f"accumulate N={N}")
