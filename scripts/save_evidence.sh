@@ -29,7 +29,7 @@ python3 - "$TAG" <<'EOF'
 import json, re, sys
 tag = sys.argv[1]
 def kib(path, ctr, acc="false"):
-    # acc: the accumulating instantiation (configs[3]'s row tiles) is <long, 2, 8, true, true, false>
+    # acc: the accumulating instantiation (configs[3]'s row tiles) is <long, 2, 4, true, true, false, true>
     txt = open(f"profiles/{tag}/{path}").read()
     # the pipelined kernel since round 6: <long, 2, 4, SMALL_M, ACC, FLAG, PIPE>
     m = re.search(r"combine_exact_kernel<long, 2, 4, true, " + acc + r", false, true>\n\s+" + ctr + r"\s+([0-9.e+]+)", txt)
