@@ -213,7 +213,7 @@ def cpu_baseline_chacha(threads: int, budget_s: float):
 
 def multi_device_leg(args):
     """The drop-in boundary over every GPU of the node from ONE process (sda_engine_create_multi):
-    runs in a child process (started before this one touches a GPU; killed after 300 s) and returns its record,
+    runs in a child process (started before this one touches a GPU; killed after 150 s: a first cross-device RCCL run that hangs must not hold up the line) and returns its record,
     or None with one visible GPU.  SDA_BENCH_MULTI_DEVICES="0,0" rehearses it on one GPU (slices on one device)."""
     import subprocess
     forced = os.environ.get("SDA_BENCH_MULTI_DEVICES")
@@ -228,9 +228,9 @@ def multi_device_leg(args):
     cmd = [sys.executable, os.path.abspath(__file__), "--multi-device-leg", devs, "--rows", str(args.rows),
            "--dim", str(args.dim)]
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=150)
     except subprocess.TimeoutExpired:
-        return {"error": "timed out after 300 s", "devices": devs}
+        return {"error": "timed out after 150 s", "devices": devs}
     sys.stderr.write(r.stderr[-4000:])
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     if r.returncode != 0 or not lines:
