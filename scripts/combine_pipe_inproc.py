@@ -3,7 +3,8 @@ round 6's tuning the knob also took the depths 2 / 4 / 6 / 8, profiles/r06m): on
 10k x 1M i64 buffer, the variants interleaved launch block by launch block, HIP events on the launch stream, so
 buffer placement and box state are shared by every variant.  Also checks the variants agree bit for bit.
     python scripts/combine_pipe_inproc.py [rounds] [variants ...]
-SDA_INPROC_SHAPE=acc times the accumulating kernel on configs[3]'s 1000 x 10M tile instead.
+SDA_INPROC_SHAPE=acc times the accumulating kernel on configs[3]'s 1000 x 10M tile instead; SDA_INPROC_KNOB names
+the variable the variants set (default SDA_COMBINE_PIPE; e.g. SDA_COMBINE_BALANCE).
 """
 import os
 import sys
@@ -16,6 +17,7 @@ from sda_amd import Engine  # noqa: E402
 M = 2147482801
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 variants = sys.argv[2:] or ["0", "1"]
+knob = os.environ.get("SDA_INPROC_KNOB", "SDA_COMBINE_PIPE")
 torch.cuda.init()
 eng = Engine(0)
 acc = os.environ.get("SDA_INPROC_SHAPE") == "acc"
@@ -36,7 +38,7 @@ def launch(v):
 res = {v: [] for v in variants}
 for r in range(rounds):
     for v in variants:
-        os.environ["SDA_COMBINE_PIPE"] = v
+        os.environ[knob] = v
         launch(v)                                                                   # warm
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -46,9 +48,9 @@ for r in range(rounds):
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 10
         res[v].append(ms)
-        print(f"round {r} PIPE={v} {ms:.4f} ms  {8.0 * N * D / ms / 1e9:.3f} TB/s", flush=True)
+        print(f"round {r} {knob}={v} {ms:.4f} ms  {8.0 * N * D / ms / 1e9:.3f} TB/s", flush=True)
 same = all(torch.equal(outs[v], outs[variants[0]]) for v in variants)
 for v in variants:
     s = sorted(res[v])
-    print(f"PIPE={v}: median {s[len(s) // 2]:.4f} ms, min {s[0]:.4f}, max {s[-1]:.4f}")
+    print(f"{knob}={v}: median {s[len(s) // 2]:.4f} ms, min {s[0]:.4f}, max {s[-1]:.4f}")
 print("bit-identical across variants:", same)

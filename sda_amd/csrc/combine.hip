@@ -47,10 +47,21 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict_
                                                             uint64_t n, uint64_t n_lanes,
                                                             uint64_t stride,
                                                             int64_t* __restrict__ out, Mod64 M,
-                                                            int64_t* __restrict__ flags = nullptr) {
+                                                            int64_t* __restrict__ flags = nullptr,
+                                                            uint32_t wlo = 0, uint32_t nwide = 0) {
     typedef typename vec_t<T, VEC>::type V;
     // (natural workgroup order: the XCD-chunked order of xcd.h measured neutral here, profiles/r04b)
-    const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // wlo > 0: balanced grid (combine_grid) -- workgroup g owns wlo lanes (+ 8 for the first nwide workgroups),
+    // starting at g wlo + 8 min(g, nwide): multiples of 8 lanes, so every wave segment stays 128-byte aligned
+    uint64_t lane;
+    if (wlo) {
+        const uint64_t g = blockIdx.x;
+        const uint32_t width = wlo + (g < nwide ? 8u : 0u);
+        if (threadIdx.x >= width) return;
+        lane = g * wlo + 8 * (g < nwide ? g : (uint64_t)nwide) + threadIdx.x;
+    } else {
+        lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    }
     if (lane >= n_lanes) return;
     const V* p = reinterpret_cast<const V*>(in + lane * VEC);
     const uint64_t vstride = stride / VEC;     // stride in units of V (host guarantees divisibility)
@@ -129,17 +140,58 @@ __global__ __launch_bounds__(256) void combine_exact_kernel(const T* __restrict_
     reinterpret_cast<VO*>(out)[lane] = o;
 }
 
+// Balanced grid (the pipelined kernels' default; SDA_COMBINE_BALANCE=0 is the A/B knob): the grid is whole rounds
+// of resident workgroups and every workgroup holds (nearly) the same number of lanes, so each CU has the same work
+// to the end.  The plain grid of 256-lane workgroups left 1,954 workgroups for configs[1]'s 1M columns on 2,048
+// slots: 162 CUs ran 8 of them, 94 ran 7 and idled for the last eighth.  In one process, interleaved
+// (scripts/combine_pipe_inproc.py, profiles/r06w): 12.770 -> 12.563 ms per configs[1] launch, 13.050 -> 12.760 ms
+// per configs[3] 1000 x 10M tile; bit-identical.
+bool combine_balance() {
+    const char* e = getenv("SDA_COMBINE_BALANCE");
+    return !(e && e[0] == '0');
+}
+
+// The balanced grid of a kernel: G = whole rounds of (CUs x resident workgroups per CU) workgroups, the lanes
+// split as G wlo + 8 nwide (wlo a multiple of 8, at most 248).  false when the job is too small to fill a round.
+bool combine_grid(const void* kernel, uint64_t n_lanes, uint64_t* G, uint32_t* wlo, uint32_t* nwide) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || cus <= 0 || per_cu <= 0)
+        return false;
+    const uint64_t slots = (uint64_t)cus * (uint64_t)per_cu;
+    if (n_lanes < slots * 64) return false;
+    const uint64_t rounds = (n_lanes + slots * 256 - 1) / (slots * 256);
+    const uint64_t g = slots * rounds;
+    uint64_t lo = n_lanes / g / 8 * 8;
+    if (lo > 248) lo = 248;
+    const uint64_t wide = (n_lanes - g * lo + 7) / 8;
+    if (lo == 0 || wide > g) return false;
+    *G = g;
+    *wlo = (uint32_t)lo;
+    *nwide = (uint32_t)wide;
+    return g <= 0x7FFFFFFFull;
+}
+
 template <typename T, int VEC, int UNROLL, bool ACC, bool FLAG = false, bool PIPE = false>
 hipError_t launch_vec(const T* in, uint64_t n, uint64_t dim, uint64_t stride, int64_t* out,
                       const Mod64& M, bool small_m, hipStream_t s, int64_t* flags = nullptr) {
     const uint64_t n_lanes = dim / VEC;
-    const uint64_t blocks = (n_lanes + 255) / 256;
+    uint64_t blocks = (n_lanes + 255) / 256;
+    uint32_t wlo = 0, nwide = 0;
+    const void* k = small_m ? reinterpret_cast<const void*>(combine_exact_kernel<T, VEC, UNROLL, true, ACC, FLAG, PIPE>)
+                            : reinterpret_cast<const void*>(combine_exact_kernel<T, VEC, UNROLL, false, ACC, FLAG, PIPE>);
+    if (PIPE && combine_balance()) {
+        uint64_t g;
+        if (combine_grid(k, n_lanes, &g, &wlo, &nwide)) blocks = g;
+        else wlo = nwide = 0;
+    }
     if (small_m)
         hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, true, ACC, FLAG, PIPE>), dim3((unsigned)blocks),
-                           dim3(256), 0, s, in, n, n_lanes, stride, out, M, flags);
+                           dim3(256), 0, s, in, n, n_lanes, stride, out, M, flags, wlo, nwide);
     else
         hipLaunchKernelGGL((combine_exact_kernel<T, VEC, UNROLL, false, ACC, FLAG, PIPE>), dim3((unsigned)blocks),
-                           dim3(256), 0, s, in, n, n_lanes, stride, out, M, flags);
+                           dim3(256), 0, s, in, n, n_lanes, stride, out, M, flags, wlo, nwide);
     return hipGetLastError();
 }
 

@@ -341,3 +341,23 @@ def test_combine_pipelined_row_counts(engine, oracle, monkeypatch, pipe):
         engine.combine_accumulate_dev(m, xd[1].data_ptr(), N, D, D, acc.data_ptr(), _stream())
         torch.cuda.synchronize()
         assert_same(acc.cpu().numpy(), oracle.combine(m, x[:N + 1]), f"accumulate N={N}")
+
+
+@pytest.mark.parametrize("balance", ["1", "0"], ids=["balanced", "plain_grid"])
+@pytest.mark.parametrize("dim", [262_146, 1_048_560, 1_048_578], ids=["one_wide_wg", "widths_248_256", "two_rounds"])
+def test_combine_balanced_grid_widths(engine, oracle, monkeypatch, balance, dim):
+    """combine.hip's balanced grid (workgroups of wlo or wlo + 8 lanes, starting at g wlo + 8 min(g, nwide)) at its
+    edge cases -- a single wide workgroup, widths capped at 248 / 256 lanes, a second round of workgroups -- plain
+    and accumulating, signed inputs, against the reference recurrence on every column."""
+    monkeypatch.setenv("SDA_COMBINE_BALANCE", balance)
+    m, N = 2147482801, 9
+    x = torch.empty((N, dim), dtype=torch.int64, device="cuda")
+    engine.synth_fill_dev(x.data_ptr(), N, dim, 0x5DA + dim, -(m - 1), m, _stream())
+    out = torch.empty(dim, dtype=torch.int64, device="cuda")
+    engine.combine_dev(m, x.data_ptr(), N, dim, dim, out.data_ptr(), _stream())
+    acc = x[0].clone()
+    engine.combine_accumulate_dev(m, x[1].data_ptr(), N - 1, dim, dim, acc.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    exp = oracle.combine(m, x.cpu().numpy())
+    assert_same(out.cpu().numpy(), exp)
+    assert_same(acc.cpu().numpy(), exp)
