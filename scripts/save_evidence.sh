@@ -36,11 +36,14 @@ def kib(path, ctr, acc="false"):
     return float(m.group(1))
 import csv
 def trace_avg_ms(grid_x):
-    # the dominant combine launch's average in this session's rocprofv3 --kernel-trace (kernel_stats_by_grid.csv)
-    for r in csv.DictReader(open(f"profiles/{tag}/kernel_stats_by_grid.csv")):
-        if r["kernel"].startswith("sda::combine_exact_kernel<long, 2, 4, true, false, false, true>") and \
-                int(r["grid_x"]) == grid_x:
-            return float(r["avg_us"]) / 1e3, int(r["calls"])
+    # the dominant combine launch's average in this session's rocprofv3 --kernel-trace (kernel_stats_by_grid.csv):
+    # the plain grid (grid_x lanes rounded to 256) or, since the balanced grid, the launch shape with most calls
+    rows = [r for r in csv.DictReader(open(f"profiles/{tag}/kernel_stats_by_grid.csv"))
+            if r["kernel"].startswith("sda::combine_exact_kernel<long, 2, 4, true, false, false, true>")]
+    exact = [r for r in rows if int(r["grid_x"]) == grid_x]
+    pick = exact or sorted(rows, key=lambda r: -int(r["calls"]))[:1]
+    if pick and grid_x < 1000000:          # configs[3]'s tile is not in the default bench's trace
+        return float(pick[0]["avg_us"]) / 1e3, int(pick[0]["calls"])
     return None, 0
 untraced = json.load(open(f"profiles/{tag}/bench.json"))
 traced = json.load(open(f"profiles/{tag}/bench_traced.json"))
