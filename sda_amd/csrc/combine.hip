@@ -153,11 +153,13 @@ bool combine_balance() {
 
 // The balanced grid of a kernel: G = whole rounds of (CUs x resident workgroups per CU) workgroups, the lanes
 // split as G wlo + 8 nwide (wlo a multiple of 8, at most 248).  false when the job is too small to fill a round.
-bool combine_grid(const void* kernel, uint64_t n_lanes, uint64_t* G, uint32_t* wlo, uint32_t* nwide) {
-    int dev = 0, cus = 0, per_cu = 0;
+// (per_cu: the kernel's resident 256-lane workgroups per CU, queried once per instantiation by the caller; the
+// smallest jobs -- below 64 lanes per slot of a 256-CU part -- skip the device queries altogether)
+bool combine_grid(int per_cu, uint64_t n_lanes, uint64_t* G, uint32_t* wlo, uint32_t* nwide) {
+    if (per_cu <= 0 || n_lanes < (uint64_t)per_cu * 256 * 64) return false;
+    int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || cus <= 0 || per_cu <= 0)
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         return false;
     const uint64_t slots = (uint64_t)cus * (uint64_t)per_cu;
     if (n_lanes < slots * 64) return false;
@@ -179,11 +181,22 @@ hipError_t launch_vec(const T* in, uint64_t n, uint64_t dim, uint64_t stride, in
     const uint64_t n_lanes = dim / VEC;
     uint64_t blocks = (n_lanes + 255) / 256;
     uint32_t wlo = 0, nwide = 0;
-    const void* k = small_m ? reinterpret_cast<const void*>(combine_exact_kernel<T, VEC, UNROLL, true, ACC, FLAG, PIPE>)
-                            : reinterpret_cast<const void*>(combine_exact_kernel<T, VEC, UNROLL, false, ACC, FLAG, PIPE>);
     if (PIPE && combine_balance()) {
+        // resident workgroups per CU of this instantiation (the same on every MI355X): queried once
+        static const int per_cu_small = [] {
+            int v = 0;
+            return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                       &v, reinterpret_cast<const void*>(combine_exact_kernel<T, VEC, UNROLL, true, ACC, FLAG, PIPE>),
+                       256, 0) == hipSuccess ? v : 0;
+        }();
+        static const int per_cu_big = [] {
+            int v = 0;
+            return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                       &v, reinterpret_cast<const void*>(combine_exact_kernel<T, VEC, UNROLL, false, ACC, FLAG, PIPE>),
+                       256, 0) == hipSuccess ? v : 0;
+        }();
         uint64_t g;
-        if (combine_grid(k, n_lanes, &g, &wlo, &nwide)) blocks = g;
+        if (combine_grid(small_m ? per_cu_small : per_cu_big, n_lanes, &g, &wlo, &nwide)) blocks = g;
         else wlo = nwide = 0;
     }
     if (small_m)
