@@ -1,6 +1,8 @@
 """In-process A/B of a knob of the clerk's decode -> combine (default SDA_SLOT_CPL, read per call): 1000 x 1M signed
 field-share payloads encoded once, the variants interleaved call block by call block, HIP events around 5 calls.
     python scripts/codec_inproc.py [rounds] [variants ...]        (SDA_INPROC_KNOB names the variable)
+SDA_INPROC_SHAPE=encode times the encode of the same matrix instead (varint_encode_dev, host wait included);
+SDA_INPROC_SHAPE=decode the decode of the payloads back into a 1000 x 1M i64 matrix (varint_decode_dev).
 """
 import os
 import sys
@@ -25,17 +27,40 @@ cap = N * D * 6 + 32
 buf = torch.zeros(cap, dtype=torch.uint8, device="cuda")
 rb = eng.varint_encode_dev(x.data_ptr(), N, D, D, buf.data_ptr(), cap, st)
 off = np.concatenate([[0], np.cumsum(rb)]).astype(np.uint64)
-del x
-outs = {v: torch.empty(D, dtype=torch.int64, device="cuda") for v in variants}
+enc = os.environ.get("SDA_INPROC_SHAPE") == "encode"
+dec = os.environ.get("SDA_INPROC_SHAPE") == "decode"
+if dec:
+    del x
+    mat = torch.empty((N, D), dtype=torch.int64, device="cuda")
+    outs = {v: torch.empty(D, dtype=torch.int64, device="cuda") for v in variants}
+elif enc:
+    outs = {v: torch.zeros(cap, dtype=torch.uint8, device="cuda") for v in variants}
+    del buf
+else:
+    del x
+    outs = {v: torch.empty(D, dtype=torch.int64, device="cuda") for v in variants}
+
+
+def call(v):
+    if dec:
+        eng.varint_decode_dev(buf.data_ptr(), off, mat.data_ptr(), D, st)
+        outs[v].copy_(mat[N - 1])
+    elif enc:
+        eng.varint_encode_dev(x.data_ptr(), N, D, D, outs[v].data_ptr(), cap, st)
+    else:
+        eng.clerk_decode_combine_dev(M, buf.data_ptr(), off, outs[v].data_ptr(), D, st)
+
+
+
 res = {v: [] for v in variants}
 for r in range(rounds):
     for v in variants:
         os.environ[knob] = v
-        eng.clerk_decode_combine_dev(M, buf.data_ptr(), off, outs[v].data_ptr(), D, st)        # warm
+        call(v)                                                                           # warm
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(5):
-            eng.clerk_decode_combine_dev(M, buf.data_ptr(), off, outs[v].data_ptr(), D, st)
+            call(v)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 5

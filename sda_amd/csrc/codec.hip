@@ -310,7 +310,7 @@ __device__ __forceinline__ int64_t varint_value_at(const uint32_t* lb, uint32_t 
 // out + r * kSlotCap, and the region's element count to region_count[r]; region_base and blob_irregular
 // are not read.  A region with more than kSlotCap elements sets *wide, and so does a malformed blob (a run
 // of >= 11 continuation bytes always holds an element longer than 5 bytes).
-template <typename OutT, bool SPARSE = false>
+template <typename OutT, bool SPARSE = false, bool NT = false>
 __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* __restrict__ bytes,
                                                                  const uint64_t* __restrict__ blob_region,
                                                                  const uint64_t* __restrict__ blob_off, uint32_t y0,
@@ -408,11 +408,14 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
                 const uint32_t g4 = len == 5 ? (b1 & 0x7Fu) : 0u;
                 narrow_fail |= len > 5 || g4 > 15;
                 const uint32_t zl = x | (g4 << 28);
-                dst[base + i] = (OutT)((zl >> 1) ^ (0u - (zl & 1u)));
+                const OutT val = (OutT)((zl >> 1) ^ (0u - (zl & 1u)));
+                if constexpr (NT) __builtin_nontemporal_store(val, dst + base + i);
+                else dst[base + i] = val;
                 continue;
             }
-            const int64_t val = varint_value_at(lb, P, len);
-            dst[base + i] = (OutT)val;
+            const OutT val = (OutT)varint_value_at(lb, P, len);
+            if constexpr (NT) __builtin_nontemporal_store(val, dst + base + i);
+            else dst[base + i] = val;
         }
         base += total;
     }
@@ -425,6 +428,16 @@ __global__ __launch_bounds__(kThreads) void varint_decode_kernel(const uint8_t* 
             if (base > kSlotCap) atomicOr(wide, 1u);
         }
     }
+}
+
+// Nontemporal element stores for the clerk's slots (SPARSE): decode -> combine -1.5 % in-process (2.625 ->
+// 2.586 ms at 1000 x 1M); the i64 matrix decode ran 3.5 % slower with them (3.288 -> 3.403 ms) and keeps cached
+// stores (profiles/r06ae).  SDA_DEC_NT (read per call; A/B knob) = 0 / 1 forces cached / nontemporal everywhere.
+template <typename OutT, bool SPARSE = false>
+static auto dec_kernel() {
+    const char* e = getenv("SDA_DEC_NT");
+    const bool nt = e && (e[0] == '0' || e[0] == '1') ? e[0] == '1' : SPARSE;
+    return nt ? varint_decode_kernel<OutT, SPARSE, true> : varint_decode_kernel<OutT, SPARSE, false>;
 }
 
 // ---------------- the clerk's decode -> combine over region slots ----------------
@@ -900,6 +913,7 @@ __device__ __forceinline__ uint64_t leb_spread8(uint64_t z) {
 // the ends (shared with the neighbouring chunks) are written byte-wise.
 // Chunk (c, row) starts at dst + row_base[row] + chunk_off (the exclusive scan of the row's chunk_bytes);
 // nothing is written when *too_big (the rows do not fit dst_cap).
+template <bool NT>
 __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* __restrict__ vals, uint64_t len,
                                                                 uint64_t stride, uint32_t chunks,
                                                                 const uint64_t* __restrict__ chunk_off,
@@ -993,7 +1007,9 @@ __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* _
     for (uint32_t k = threadIdx.x; k < nq; k += kThreads) {
         const uint32_t lo = k * 16, hi = lo + 16;
         if (lo >= lead && hi <= end) {
-            d128[k] = buf4[k];
+            if constexpr (NT)
+                __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(buf4)[k], reinterpret_cast<u32x4*>(d128) + k);
+            else d128[k] = buf4[k];
         } else {
             for (uint32_t i = lo; i < hi; ++i)
                 if (i >= lead && i < end) d8[i] = b8[i];
@@ -1144,9 +1160,9 @@ hipError_t launch_varint_decode(const uint8_t* bytes, uint64_t n_blobs, const Va
     hipError_t e;
     for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
         const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
-        hipLaunchKernelGGL(varint_decode_kernel<int64_t>, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s,
+        hipLaunchKernelGGL(dec_kernel<int64_t>(), dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s,
                            bytes, w.blob_region, w.blob_off, (uint32_t)y0, w.region_base, w.irregular, out, out_stride,
-                           w.wide);
+                           w.wide, (uint32_t*)nullptr, (const uint32_t*)nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (irregular_any) {
@@ -1185,7 +1201,7 @@ hipError_t launch_varint_decode_one_wait(const uint8_t* bytes, const uint64_t* b
     if ((e = hipGetLastError()) != hipSuccess) return e;
     for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
         const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
-        hipLaunchKernelGGL(varint_decode_kernel<int64_t>, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s,
+        hipLaunchKernelGGL(dec_kernel<int64_t>(), dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s,
                            bytes, w.blob_region, w.blob_off, (uint32_t)y0, w.region_base, w.irregular, out, out_stride,
                            (uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)w.wide);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1210,9 +1226,9 @@ hipError_t launch_varint_decode_narrow(const uint8_t* bytes, uint64_t n_blobs, c
     if ((e = hipMemsetAsync(w.wide, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
     for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
         const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
-        hipLaunchKernelGGL(varint_decode_kernel<int32_t>, dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s,
+        hipLaunchKernelGGL(dec_kernel<int32_t>(), dim3((unsigned)plan.max_regions, ny), dim3(kThreads), 0, s,
                            bytes, w.blob_region, w.blob_off, (uint32_t)y0, w.region_base, w.irregular, out, out_stride,
-                           w.wide);
+                           w.wide, (uint32_t*)nullptr, (const uint32_t*)nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     uint32_t flag = 0;
@@ -1297,10 +1313,10 @@ hipError_t launch_varint_decode_slots_combine(const uint8_t* bytes, const uint64
             const uint64_t g1 = g0 + sg.G < n_blobs ? g0 + sg.G : n_blobs;
             const uint64_t ng = g1 - g0, R0 = plan.blob_region[g0];
             if (plan.blob_region[g1] > R0) {
-                hipLaunchKernelGGL((varint_decode_kernel<int32_t, true>), dim3((unsigned)plan.max_regions, (unsigned)ng),
+                hipLaunchKernelGGL((dec_kernel<int32_t, true>()), dim3((unsigned)plan.max_regions, (unsigned)ng),
                                    dim3(kThreads), 0, s, bytes, w.blob_region, w.blob_off, (uint32_t)g0,
                                    (const uint64_t*)nullptr, (const uint32_t*)nullptr, slots - R0 * kSlotCap, 0, w.wide,
-                                   w.region_count);
+                                   w.region_count, (const uint32_t*)nullptr);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
             }
             hipLaunchKernelGGL(varint_scan_kernel, dim3((unsigned)ng), dim3(kThreads), 0, s, w.region_count,
@@ -1329,9 +1345,9 @@ hipError_t launch_varint_decode_slots_combine(const uint8_t* bytes, const uint64
     }
     for (uint64_t y0 = 0; R && y0 < n_blobs; y0 += 65535) {
         const unsigned ny = (unsigned)(n_blobs - y0 < 65535 ? n_blobs - y0 : 65535);
-        hipLaunchKernelGGL((varint_decode_kernel<int32_t, true>), dim3((unsigned)plan.max_regions, ny), dim3(kThreads),
+        hipLaunchKernelGGL((dec_kernel<int32_t, true>()), dim3((unsigned)plan.max_regions, ny), dim3(kThreads),
                            0, s, bytes, w.blob_region, w.blob_off, (uint32_t)y0, (const uint64_t*)nullptr,
-                           (const uint32_t*)nullptr, slots, 0, w.wide, w.region_count);
+                           (const uint32_t*)nullptr, slots, 0, w.wide, w.region_count, (const uint32_t*)nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(varint_scan_kernel, dim3((unsigned)n_blobs), dim3(kThreads), 0, s, w.region_count,
@@ -1425,9 +1441,17 @@ hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len
     hipLaunchKernelGGL(varint_rows_kernel, dim3(1), dim3(kThreads), 0, s, (const uint64_t*)rbytes, rows, dst_cap,
                        row_base, too_big);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(varint_write_kernel, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s, vals, len,
-                       stride, (uint32_t)chunks, (const uint64_t*)chunk_off, (const uint64_t*)row_base,
-                       (const uint32_t*)too_big, dst);
+    // nontemporal payload stores: encode -5.5 % in-process (3.770 -> 3.563 ms at 1000 x 1M, profiles/r06ad);
+    // SDA_ENC_NT=0 (read per call) keeps cached stores for A/B
+    const char* nt = getenv("SDA_ENC_NT");
+    if (!(nt && nt[0] == '0'))
+        hipLaunchKernelGGL(varint_write_kernel<true>, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s,
+                           vals, len, stride, (uint32_t)chunks, (const uint64_t*)chunk_off,
+                           (const uint64_t*)row_base, (const uint32_t*)too_big, dst);
+    else
+        hipLaunchKernelGGL(varint_write_kernel<false>, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s,
+                           vals, len, stride, (uint32_t)chunks, (const uint64_t*)chunk_off,
+                           (const uint64_t*)row_base, (const uint32_t*)too_big, dst);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipMemcpyAsync(row_bytes_host, rbytes, rows * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
