@@ -25,6 +25,7 @@ x = torch.empty((N, D), dtype=torch.int64, device="cuda")
 eng.synth_fill_dev(x.data_ptr(), N, D, 0x5DA + 6, -(M - 1), M, st)
 cap = N * D * 6 + 32
 buf = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+ecap = N * D * 10              # the encode shape: room for any i64 (the one-pass encode's condition)
 rb = eng.varint_encode_dev(x.data_ptr(), N, D, D, buf.data_ptr(), cap, st)
 off = np.concatenate([[0], np.cumsum(rb)]).astype(np.uint64)
 enc = os.environ.get("SDA_INPROC_SHAPE") == "encode"
@@ -34,8 +35,8 @@ if dec:
     mat = torch.empty((N, D), dtype=torch.int64, device="cuda")
     outs = {v: torch.empty(D, dtype=torch.int64, device="cuda") for v in variants}
 elif enc:
-    outs = {v: torch.zeros(cap, dtype=torch.uint8, device="cuda") for v in variants}
     del buf
+    outs = {v: torch.zeros(ecap, dtype=torch.uint8, device="cuda") for v in variants}
 else:
     del x
     outs = {v: torch.empty(D, dtype=torch.int64, device="cuda") for v in variants}
@@ -46,7 +47,7 @@ def call(v):
         eng.varint_decode_dev(buf.data_ptr(), off, mat.data_ptr(), D, st)
         outs[v].copy_(mat[N - 1])
     elif enc:
-        eng.varint_encode_dev(x.data_ptr(), N, D, D, outs[v].data_ptr(), cap, st)
+        eng.varint_encode_dev(x.data_ptr(), N, D, D, outs[v].data_ptr(), ecap, st)
     else:
         eng.clerk_decode_combine_dev(M, buf.data_ptr(), off, outs[v].data_ptr(), D, st)
 
