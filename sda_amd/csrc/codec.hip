@@ -913,54 +913,23 @@ __device__ __forceinline__ uint64_t leb_spread8(uint64_t z) {
 // the ends (shared with the neighbouring chunks) are written byte-wise.
 // Chunk (c, row) starts at dst + row_base[row] + chunk_off (the exclusive scan of the row's chunk_bytes);
 // nothing is written when *too_big (the rows do not fit dst_cap).
-//
-// ONEPASS: no size pass.  Each workgroup takes the next chunk in (row, chunk) order from a ticket counter,
-// counts its bytes from the values already in registers, and finds its global byte offset by a decoupled
-// look-back over the chunks before it (one status word each: aggregate, or inclusive prefix once known).  A
-// chunk waits only on chunks that took their tickets earlier, so they are running and publish their aggregate
-// without waiting themselves; the wait is bounded anyway (kLbSpinCap polls), and a chunk that gives up sets
-// op.err, writes nothing and publishes a prefix, so every later chunk still finishes and the host reruns the
-// three-pass encode.  Rows end up back to back exactly as in the three-pass form.
-struct EncOnePass {
-    uint32_t* ticket;        // zeroed before the launch
-    uint64_t* state;         // [rows * chunks] status words, zeroed before the launch
-    uint64_t* chunk_start;   // [rows * chunks] each chunk's byte offset from dst
-    uint32_t* err;           // zeroed before the launch
-    uint64_t cap;            // dst_cap: a chunk that would end past it writes nothing and sets err
-};
-constexpr uint64_t kLbAgg = 1ull << 62, kLbPre = 2ull << 62, kLbVal = kLbAgg - 1;
-constexpr uint32_t kLbSpinCap = 1u << 22;
-
-template <bool NT, bool ONEPASS = false>
+template <bool NT>
 __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* __restrict__ vals, uint64_t len,
                                                                 uint64_t stride, uint32_t chunks,
                                                                 const uint64_t* __restrict__ chunk_off,
                                                                 const uint64_t* __restrict__ row_base,
                                                                 const uint32_t* __restrict__ too_big,
-                                                                uint8_t* __restrict__ dst, EncOnePass op) {
-    uint32_t c, row;
-    __shared__ uint32_t s_ticket;
-    if constexpr (ONEPASS) {
-        if (op.ticket) {                                     // ticket order (SDA_ENC_ONEPASS=1)
-            if (threadIdx.x == 0) s_ticket = atomicAdd(op.ticket, 1u);
-            __syncthreads();
-        } else if (threadIdx.x == 0) {                       // dispatch order (workgroup id)
-            s_ticket = blockIdx.x;
-        }
-        __syncthreads();
-        c = s_ticket % chunks;
-        row = s_ticket / chunks;
-    } else {
-        c = blockIdx.x;
-        row = blockIdx.y;
-        if (*too_big) return;
-    }
+                                                                uint8_t* __restrict__ dst) {
+    const uint32_t c = blockIdx.x, row = blockIdx.y;
+    if (*too_big) return;
     const uint64_t e0 = (uint64_t)c * kEncChunk;
     constexpr uint32_t kBufQuads = (kEncChunk * 10 + 32) / 16;      // lead < 16, + the shifted tail dwords
     __shared__ uint4 buf4[kBufQuads];
     __shared__ uint32_t wsum[kThreads / 64];
     uint32_t* buf = reinterpret_cast<uint32_t*>(buf4);
     const uint8_t* b8 = reinterpret_cast<const uint8_t*>(buf4);
+    uint8_t* gdst = dst + row_base[row] + chunk_off[(uint64_t)row * chunks + c];
+    const uint32_t lead = (uint32_t)((uintptr_t)gdst & 15);
     for (uint32_t k = threadIdx.x; k < kBufQuads; k += kThreads) buf4[k] = make_uint4(0, 0, 0, 0);
     // round q: lane t owns the kEncEpl adjacent elements e0 + R q + kEncEpl t + j (R = kEncEpl * 256;
     // 16-byte loads when the chunk allows it), so one block-wide scan of the lane sizes places R elements
@@ -985,71 +954,6 @@ __global__ __launch_bounds__(kThreads) void varint_write_kernel(const int64_t* _
                 v[q][j] = e < len ? rowp[e] : 0;
             }
     }
-    uint8_t* gdst;
-    if constexpr (ONEPASS) {
-        uint32_t nb = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < kEncRounds; ++q)
-#pragma unroll
-            for (uint32_t j = 0; j < kEncEpl; ++j)
-                nb += e0 + kEncEpl * (q * kThreads + threadIdx.x) + j < len ? varint_size(v[q][j]) : 0u;
-        nb = wave_incl_scan(nb);
-        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = nb;
-        __syncthreads();
-        // the whole workgroup looks back over a window of 256 chunks per poll (a window of 64 measured the
-        // prefix chain as the limit)
-        __shared__ unsigned long long lb_sum[kThreads / 64];
-        __shared__ uint32_t lb_first[kThreads / 64];
-        const uint32_t t = s_ticket, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        uint64_t total = 0, excl = 0;
-        for (uint32_t w = 0; w < kThreads / 64; ++w) total += wsum[w];
-        bool fail = false;
-        if (t > 0) {
-            if (threadIdx.x == 0)
-                __hip_atomic_store(op.state + t, kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int64_t look = (int64_t)t - 1;
-            uint32_t spins = 0;
-            for (;;) {
-                const int64_t idx = look - (int64_t)threadIdx.x;
-                const uint64_t w = idx >= 0 ? __hip_atomic_load(op.state + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                            : kLbPre;            // before the first chunk: prefix 0
-                const uint32_t st = (uint32_t)(w >> 62);
-                if (__syncthreads_or(st == 0)) {                 // a chunk in the window has not published yet
-                    if (++spins > kLbSpinCap) {
-                        fail = true;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                const unsigned long long pm = __ballot(st == 2);
-                if (lane == 0) lb_first[wv] = pm ? wv * 64 + (uint32_t)__builtin_ctzll(pm) : kThreads;
-                __syncthreads();
-                uint32_t first = kThreads;                       // the nearest inclusive prefix in the window
-                for (uint32_t q = 0; q < kThreads / 64; ++q) first = lb_first[q] < first ? lb_first[q] : first;
-                unsigned long long x = threadIdx.x <= first ? (w & kLbVal) : 0ull;
-                for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-                if (lane == 0) lb_sum[wv] = x;
-                __syncthreads();
-                for (uint32_t q = 0; q < kThreads / 64; ++q) excl += lb_sum[q];
-                __syncthreads();                                 // lb_first / lb_sum are rewritten next poll
-                if (first < kThreads) break;
-                look -= kThreads;
-            }
-        }
-        fail = fail || excl + total > op.cap;
-        if (threadIdx.x == 0) {
-            __hip_atomic_store(op.state + t, kLbPre | ((excl + total) & kLbVal), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            op.chunk_start[t] = excl;
-            if (fail) atomicOr(op.err, 1u);
-        }
-        if (fail) return;
-        gdst = dst + excl;
-    } else {
-        gdst = dst + row_base[row] + chunk_off[(uint64_t)row * chunks + c];
-    }
-    const uint32_t lead = (uint32_t)((uintptr_t)gdst & 15);
     uint32_t base = lead;
 #pragma unroll
     for (uint32_t q = 0; q < kEncRounds; ++q) {
@@ -1163,18 +1067,6 @@ __global__ __launch_bounds__(kThreads) void varint_offsets_kernel(const uint64_t
         __syncthreads();
     }
     if (threadIdx.x == 0 && row_bytes) row_bytes[row] = total;
-}
-
-// ONEPASS: each row's byte count from its first chunk's offset and the next row's (the last row ends at the
-// last chunk's inclusive prefix)
-__global__ __launch_bounds__(kThreads) void varint_rowbytes_kernel(const uint64_t* __restrict__ chunk_start,
-                                                                   const uint64_t* __restrict__ state, uint64_t rows,
-                                                                   uint32_t chunks, uint64_t* __restrict__ row_bytes) {
-    const uint64_t r = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (r >= rows) return;
-    const uint64_t start = chunk_start[r * chunks];
-    const uint64_t end = r + 1 < rows ? chunk_start[(r + 1) * chunks] : (state[rows * chunks - 1] & kLbVal);
-    row_bytes[r] = end - start;
 }
 
 }  // namespace
@@ -1521,12 +1413,11 @@ hipError_t launch_varint_decode_combine(const uint8_t* bytes, uint64_t n_blobs, 
 
 size_t varint_encode_work_bytes(uint64_t rows, uint64_t len) {
     const uint64_t chunks = (len + kEncChunk - 1) / kEncChunk;
-    return 2 * rows * (chunks ? chunks : 1) * 8 + 2 * rows * 8 + 1024 + 256;   // + too_big, ticket, err (ONEPASS)
+    return 2 * rows * (chunks ? chunks : 1) * 8 + 2 * rows * 8 + 1024 + 256;
 }
 
 hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len, uint64_t stride, uint8_t* dst,
-                                uint64_t dst_cap, void* work, uint64_t* row_bytes_host, hipStream_t s,
-                                uint32_t max_elem_bytes) {
+                                uint64_t dst_cap, void* work, uint64_t* row_bytes_host, hipStream_t s) {
     const uint64_t chunks = (len + kEncChunk - 1) / kEncChunk;
     if (rows == 0) return hipSuccess;
     uint64_t* chunk_bytes = static_cast<uint64_t*>(work);
@@ -1539,42 +1430,6 @@ hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len
         for (uint64_t r = 0; r < rows; ++r) row_bytes_host[r] = 0;
         return hipSuccess;
     }
-    // nontemporal payload stores: encode -5.5 % in-process (3.770 -> 3.563 ms at 1000 x 1M, profiles/r06ad);
-    // SDA_ENC_NT=0 (read per call) keeps cached stores for A/B
-    const char* ntv = getenv("SDA_ENC_NT");
-    const bool nt = !(ntv && ntv[0] == '0');
-    // One pass (no size pass, ONEPASS above) when the encoding cannot exceed dst_cap (max_elem_bytes per element),
-    // so "nothing is written when the rows do not fit" still holds.  The kernel also refuses to write a chunk past
-    // dst_cap (then the three passes below run and report it), so a wrong bound cannot write out of bounds.
-    // SDA_ENC_ONEPASS=0 (read per call) keeps the three passes for A/B.
-    const char* opv = getenv("SDA_ENC_ONEPASS");
-    const uint64_t nchunk = rows * chunks;
-    const uint64_t meb = max_elem_bytes < 1 ? 1 : (max_elem_bytes > 10 ? 10 : max_elem_bytes);
-    if (!(opv && opv[0] == '0') && nchunk < (1ull << 31) && len <= UINT64_MAX / 10 / rows &&
-        dst_cap >= rows * len * meb) {
-        const EncOnePass op{opv && opv[0] == '1' ? too_big + 1 : nullptr, chunk_bytes, chunk_off, too_big + 2, dst_cap};
-        if ((e = hipMemsetAsync(chunk_bytes, 0, nchunk * 8, s)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(too_big, 0, 16, s)) != hipSuccess) return e;
-        if (nt)
-            hipLaunchKernelGGL((varint_write_kernel<true, true>), dim3((unsigned)nchunk), dim3(kThreads), 0, s, vals,
-                               len, stride, (uint32_t)chunks, (const uint64_t*)nullptr, (const uint64_t*)nullptr,
-                               (const uint32_t*)too_big, dst, op);
-        else
-            hipLaunchKernelGGL((varint_write_kernel<false, true>), dim3((unsigned)nchunk), dim3(kThreads), 0, s, vals,
-                               len, stride, (uint32_t)chunks, (const uint64_t*)nullptr, (const uint64_t*)nullptr,
-                               (const uint32_t*)too_big, dst, op);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL(varint_rowbytes_kernel, dim3((unsigned)((rows + kThreads - 1) / kThreads)), dim3(kThreads),
-                           0, s, (const uint64_t*)chunk_off, (const uint64_t*)chunk_bytes, rows, (uint32_t)chunks,
-                           rbytes);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        uint32_t err = 0;
-        if ((e = hipMemcpyAsync(row_bytes_host, rbytes, rows * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-        if ((e = hipMemcpyAsync(&err, op.err, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        if (!err) return hipSuccess;
-        // a look-back gave up, or the bound was wrong (neither seen): the three passes below redo every row
-    }
     hipLaunchKernelGGL(varint_size_kernel, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s, vals, len,
                        stride, (uint32_t)chunks, chunk_bytes);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1586,14 +1441,17 @@ hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len
     hipLaunchKernelGGL(varint_rows_kernel, dim3(1), dim3(kThreads), 0, s, (const uint64_t*)rbytes, rows, dst_cap,
                        row_base, too_big);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (nt)
-        hipLaunchKernelGGL((varint_write_kernel<true>), dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s,
+    // nontemporal payload stores: encode -5.5 % in-process (3.770 -> 3.563 ms at 1000 x 1M, profiles/r06ad);
+    // SDA_ENC_NT=0 (read per call) keeps cached stores for A/B
+    const char* nt = getenv("SDA_ENC_NT");
+    if (!(nt && nt[0] == '0'))
+        hipLaunchKernelGGL(varint_write_kernel<true>, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s,
                            vals, len, stride, (uint32_t)chunks, (const uint64_t*)chunk_off,
-                           (const uint64_t*)row_base, (const uint32_t*)too_big, dst, EncOnePass{});
+                           (const uint64_t*)row_base, (const uint32_t*)too_big, dst);
     else
-        hipLaunchKernelGGL((varint_write_kernel<false>), dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s,
+        hipLaunchKernelGGL(varint_write_kernel<false>, dim3((unsigned)chunks, (unsigned)rows), dim3(kThreads), 0, s,
                            vals, len, stride, (uint32_t)chunks, (const uint64_t*)chunk_off,
-                           (const uint64_t*)row_base, (const uint32_t*)too_big, dst, EncOnePass{});
+                           (const uint64_t*)row_base, (const uint32_t*)too_big, dst);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipMemcpyAsync(row_bytes_host, rbytes, rows * 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;

@@ -1889,12 +1889,8 @@ sda_status sda_participant_share_dev(sda_engine* h, const sda_masking_scheme* ms
         if (payload) {
             if (sda_status e = ensure(&h->codec_work, &h->codec_work_bytes, sda::varint_encode_work_bytes(n, B)))
                 return e;
-            // every packed share is a result of tss' `% p` (additive shares copy the caller's draws verbatim), so
-            // with 0 < p <= 2^31 its zigzag form is below 2^32: at most 5 bytes, and a payload_cap of 5 bytes per
-            // share runs the one-pass encode
-            const bool five = packed && ss->modulus > 0 && ss->modulus <= (1ll << 31);
             hipError_t e = sda::launch_varint_encode(shares_out, n, B, B, payload, payload_cap, h->codec_work,
-                                                     payload_row_bytes, st, five ? 5u : 10u);
+                                                     payload_row_bytes, st);
             if (e == hipErrorInvalidValue) return fail(SDA_ERR_INVALID_ARGUMENT, "payload_cap too small");
             HIP_TRY(e);
         }

@@ -160,11 +160,8 @@ hipError_t launch_varint_decode_slots_combine(const uint8_t* bytes, const uint64
 size_t varint_encode_work_bytes(uint64_t rows, uint64_t len);
 // encode rows [rows][stride] (first len elements) back to back into dst; row_bytes_host gets each
 // row's byte count (synchronous).  hipErrorInvalidValue if dst_cap is too small.
-// max_elem_bytes: a bound on any element's encoded length the caller can vouch for (10 for arbitrary i64;
-// 5 for results of `% m` with m <= 2^31).  With dst_cap >= rows * len * max_elem_bytes the encode runs in one pass.
 hipError_t launch_varint_encode(const int64_t* vals, uint64_t rows, uint64_t len, uint64_t stride, uint8_t* dst,
-                                uint64_t dst_cap, void* work, uint64_t* row_bytes_host, hipStream_t s,
-                                uint32_t max_elem_bytes = 10);
+                                uint64_t dst_cap, void* work, uint64_t* row_bytes_host, hipStream_t s);
 
 // ---- chacha.hip ----
 // Combine of n_seeds ChaCha mask streams (chacha.rs:57-76), two implementations:

@@ -234,33 +234,6 @@ def test_slot_cap_overflow_falls_back(engine, oracle, monkeypatch, case):
         assert_same(res.cpu().numpy(), exp, f"{case} {path}")
 
 
-@pytest.mark.parametrize("N,D,pad", [(1, 1, 0), (3, 2048, 0), (5, 2049, 1), (7, 70_001, 3), (300, 4097, 0),
-                                     (64, 100_003, 0)])
-def test_encode_dev_one_pass_equals_three_passes(engine, oracle, monkeypatch, N, D, pad):
-    """With dst_cap >= 10 bytes per element the encode runs in one pass (chunk offsets by look-back over a
-    ticket order); its bytes and row sizes equal the three-pass encode's and the oracle's, every row, and
-    nothing past the rows is touched.  Mixed byte lengths (1..10), ragged and unaligned rows."""
-    rng = np.random.default_rng(N * 7919 + D)
-    x = _values(rng, N * (D + pad)).reshape(N, D + pad)
-    xd = torch.as_tensor(x).cuda()
-    cap = N * D * 10
-    got = {}
-    for onepass in ("1", "0"):
-        monkeypatch.setenv("SDA_ENC_ONEPASS", onepass)
-        buf = torch.full((cap + 64,), 0xA5, dtype=torch.uint8, device="cuda")
-        rb = engine.varint_encode_dev(xd.data_ptr(), N, D, D + pad, buf.data_ptr(), cap)
-        torch.cuda.synchronize()
-        got[onepass] = (np.asarray(rb).tolist(), buf.cpu().numpy())
-    assert got["1"][0] == got["0"][0]
-    total = int(sum(got["1"][0]))
-    assert (got["1"][1][:total] == got["0"][1][:total]).all()
-    assert (got["1"][1][total:] == 0xA5).all()
-    host = got["1"][1].tobytes()
-    off = np.concatenate([[0], np.cumsum(got["1"][0])]).astype(np.int64)
-    for i in range(N):
-        assert host[off[i]:off[i + 1]] == oracle.varint_encode(x[i, :D]), f"row {i}"
-
-
 def test_encode_dev_capacity(engine, oracle):
     """The encode places its rows on the device; a dst_cap one byte short of the rows' total is refused
     (ERR_INVALID_ARGUMENT) with nothing written, and the exact capacity works."""
