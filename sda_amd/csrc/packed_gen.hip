@@ -150,6 +150,9 @@ constexpr int gen_block() { return L <= 16 ? 256 : (L == 32 ? 128 : 64); }
 // Tile inputs staged by LDS DMA (global_load_lds_dwordx4) instead of loads into registers + ds_write:
 // share-gen 7.01-7.02 -> 6.96-6.99 ms exact, 6.52-6.56 -> 6.44-6.48 ms canonical (profiles/r05u).  On in every
 // object since round 6 ("LDS-DMA staging"); SDA_GEN_DMA = 0 is the A/B knob.
+#ifndef SDA_GEN_DMA_AUX
+#define SDA_GEN_DMA_AUX 2    // the DMA loads are nontemporal (exact share-gen -1.0 %, profiles/r06aj); 0 = cached (A/B)
+#endif
 #ifndef SDA_GEN_DMA
 #define SDA_GEN_DMA 1
 #endif
@@ -303,7 +306,8 @@ void packed_gen_kernel(const int64_t* __restrict__ secrets, uint64_t D, const in
                 const uint32_t nsc = 2 * k, nc = 2 * (k + t);    // 1 KiB chunks: BS k * 8 / 1024 = 2 k
                 for (uint32_t c = w; c < nc; c += BS / 64) {
                     const int64_t* src = c < nsc ? sblk + (uint64_t)c * 128 : dblk + (uint64_t)(c - nsc) * 128;
-                    __builtin_amdgcn_global_load_lds((const void*)(src + 2 * l), lbase + c * 1024, 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const void*)(src + 2 * l), lbase + c * 1024, 16, 0,
+                                                     SDA_GEN_DMA_AUX);
                 }
                 // the LDS writes of a DMA count in vmcnt, and s_barrier does not wait for them: every wave drains
                 // its own DMAs before the barrier, so the other waves' reads see every chunk
