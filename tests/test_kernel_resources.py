@@ -129,3 +129,11 @@ def test_lds_dma_stage_issues_every_chunk_before_one_wait(kernels, tmp_path):
             assert any("vmcnt(0)" in l for l in body[dma[-1]:bar]), name
             hits += 1
     assert hits == 2
+
+
+def test_reveal_kernels_have_no_static_lds(kernels):
+    """The staged reveal flush reads its results back from the dynamic LDS base as 16-byte words
+    (packed_reveal.hip, reveal_flush): that base is 16-byte aligned only while no static LDS precedes it."""
+    rows = [k for k in kernels if k["pretty"].startswith(("packed_reveal_exact_kernel<", "packed_reveal_canon_kernel<"))]
+    assert rows
+    assert all(k["lds"] == 0 for k in rows), [(k["pretty"], k["lds"]) for k in rows if k["lds"]]
